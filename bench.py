@@ -1,0 +1,236 @@
+"""Headline benchmark: env-steps/sec (agents x envs) of the fused swarm-RL training
+tick, GoTo, 8 agents x 1024 envs per GPU (BASELINE.json configs[1]; weak scaling
+to configs[3] = 8192 envs over 8 GPUs).
+
+One step = one training tick of the reference's hot loop (train_gcn_dqn.py:153-178)
+for every env of every rank: GAT Q forward on the complete graph -> ε-greedy
+(ε = 0.05) -> VMAS env.step -> replay push -> TD update on S = 1024 sampled graphs
+per rank (target fwd, online fwd, backward) -> [RCCL all-reduce of the 1,673-float
+gradient] -> clip_grad_norm_ + Adam (+ target sync every 200 ticks) -> episode reset
+every 100 ticks.  Inputs: synthetic reset states (Philox), weights
+data/models/experiment_GoTo-seed_0.pth (committed fixture), replay pre-filled with
+100 acting ticks.  Timed ticks are replayed from captured hipGraphs.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3     # MI355X FP32 MFMA (= vector) dense peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0        # HBM3E spec
+
+
+def gat_fwd_flops(N: int, avg_in_degree: float) -> float:
+    """Algorithmic FLOPs of GCN.forward per node: lin 7->32 (448), scores (128),
+    softmax (5/edge), aggregate (64/edge), bias+tanh (64), lin1 (2048+32), relu (32), lin2 (576+9)."""
+    return 448 + 128 + 69 * avg_in_degree + 64 + 2080 + 32 + 585
+
+
+def td_bwd_flops(N: int, d: float) -> float:
+    """Algorithmic FLOPs of the TD backward per sampled node."""
+    return (32 + 32 + 2048 + 96        # dR (one-hot row), relu mask, W1^T dZ, tanh'
+            + 64 * d + 8 * d + 64 * d  # g_uv, softmax/leaky backward, messages to h
+            + 128 + 128                # attention-vector terms into dh, datt
+            + 2048 + 64 + 448          # dW1, dW2 (one-hot), dW
+            + 32 * 3 + 9)              # dbias, db1, db2
+
+
+def complete_in_degree(N: int) -> float:
+    return ((N - 1) * N + 1) / N
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--scenario", default="GoTo")
+    ap.add_argument("--batch", type=int, default=None, help="sampled graphs per update per GPU (default = envs)")
+    ap.add_argument("--chunk", type=int, default=20, help="ticks per captured hipGraph")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        pg = dist.group.WORLD
+
+    import swarm_amd
+    from swarm_amd import build as swbuild
+    if rank == 0 and not swbuild.up_to_date():
+        swbuild.build()
+    if world > 1:
+        torch.distributed.barrier()
+
+    B, N = args.envs, args.agents
+    S = args.batch or B
+    scen = args.scenario
+    wkey = "weights_go_to" if scen == "GoTo" else "weights_obstacle_avoidance"
+    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
+    eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=rank * B,
+                                world_size=world, process_group=pg, update_target_every=200,
+                                replay_capacity=1_000_000)
+    max_steps = 100
+    # ---- prefill: 100 acting ticks (no learning)
+    eng.reset()
+    for _ in range(100):
+        eng.act(push=True, full_out=False)
+        eng.advance()
+    eng.reset()
+    tick_in_ep = [0]
+
+    def tick():
+        eng.train_tick(full_out=False)
+
+    chunk = max(1, math.gcd(args.steps, args.chunk)) if args.steps else 1
+    graph = None
+    if not args.no_graph and world == 1:
+        tick()                              # eager warm tick before capture
+        graph = eng.capture(chunk, tick)
+
+    def run(n):
+        done = 0
+        while done < n:
+            if tick_in_ep[0] >= max_steps:
+                eng.reset()
+                tick_in_ep[0] = 0
+            if graph is not None and n - done >= chunk and tick_in_ep[0] + chunk <= max_steps:
+                graph.replay()
+                done += chunk
+                tick_in_ep[0] += chunk
+            else:
+                tick()
+                done += 1
+                tick_in_ep[0] += 1
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ctrl = eng.read_ctrl()
+    assert ctrl["trained"] == 1 and math.isfinite(ctrl["loss"]), ctrl
+
+    # ---- per-kernel durations with HIP events on the launch stream (eager ticks)
+    kt = {}
+    if not args.no_kernel_timing:
+        stream = torch.cuda.current_stream()
+        names = ("swarm_act_step", "swarm_td_grad", "swarm_adam_step")
+        acc = {n: [] for n in names}
+        for _ in range(min(args.steps, 50)):
+            if tick_in_ep[0] >= max_steps:
+                eng.reset()
+                tick_in_ep[0] = 0
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+            ev[0].record(stream)
+            eng.act(push=True, full_out=False)
+            ev[1].record(stream)
+            ev[2].record(stream)
+            eng.td_grad()
+            ev[3].record(stream)
+            eng.allreduce_grad()
+            ev[4].record(stream)
+            eng.adam()
+            ev[5].record(stream)
+            tick_in_ep[0] += 1
+            torch.cuda.synchronize()
+            acc["swarm_act_step"].append(ev[0].elapsed_time(ev[1]) * 1e3)
+            acc["swarm_td_grad"].append(ev[2].elapsed_time(ev[3]) * 1e3)
+            acc["swarm_adam_step"].append(ev[4].elapsed_time(ev[5]) * 1e3)
+        kt = {n: float(np.mean(v)) for n, v in acc.items()}   # microseconds (td_grad includes grad_reduce)
+
+    value = B * N * world * args.steps / elapsed
+    ms = elapsed / args.steps * 1e3
+    d = complete_in_degree(N)
+    f_fwd = gat_fwd_flops(N, d)
+    td_flops_launch = S * N * (2 * f_fwd + td_bwd_flops(N, d))
+    roof = None
+    if kt:
+        t_td = kt["swarm_td_grad"] * 1e-6
+        ach = td_flops_launch / t_td / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "r01_pmc_td.json")
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        roof = {"bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": "td_kernel (swarm_td_grad)",
+                "algorithmic_flops_per_launch": td_flops_launch,
+                "algorithmic_bytes_per_launch": S * N * 37,
+                "hbm_frac": S * N * 37 / t_td / 1e9 / PEAK_HBM_GBS,
+                "kernel_us": {k: round(v, 2) for k, v in kt.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        sid = 0 if scen == "GoTo" else 1
+        r = cpu_baseline.vectorized_train(w0, sid, B, N, S, seconds=args.cpu_seconds)
+        r1 = cpu_baseline.reference_shaped_train(w0, sid, N, seconds=max(3.0, args.cpu_seconds / 3))
+        cpu = {"value": round(r["agent_steps_per_s"], 1), "unit": "agent-steps/s", "cores": threads,
+               "kind": "port",
+               "sample": f"vectorised PyTorch-CPU oracle, same workload ({B} envs x {N} agents, S={S}), "
+                         f"{r['ticks']} ticks in {r['seconds']:.1f}s on {threads} threads ({platform.processor() or 'x86_64'})",
+               "reference_shaped_b1": {"value": round(r1["agent_steps_per_s"], 1),
+                                       "sample": f"B=1 loop shaped like train_gcn_dqn.py:153-178 (S=32), "
+                                                 f"{r1['ticks']} ticks in {r1['seconds']:.1f}s"}}
+
+    if rank == 0:
+        line = {"metric": "env-steps/sec (agents×envs), GoTo 8 agents×1024 envs @1/2/4/8 GPU",
+                "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference GoTo seed_0 weights)",
+                "config": {"workload": f"{scen} train tick: {N} agents x {B} envs/GPU, GAT, complete graph, "
+                                       f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
+                           "global_envs": B * world, "td_batch_per_gpu": S, "graph": "complete",
+                           "parallelism": f"env-sharded dp{world}" + (" + RCCL grad all-reduce" if world > 1 else ""),
+                           "hipgraph": graph is not None},
+                "roofline": roof, "cpu_baseline": cpu,
+                "loss": ctrl["loss"]}
+        print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

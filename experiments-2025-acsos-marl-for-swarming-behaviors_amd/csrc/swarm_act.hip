@@ -1,0 +1,374 @@
+// swarm_act.hip — acting side of the hot path: reset, env.step, graph build,
+// GCN.forward, the fused acting tick and the multi-tick rollout.  gfx950 only.
+//
+// Reference call sites replaced (paths relative to the reference checkout):
+//   train_gcn_dqn.py:161-172   graph -> model -> eps-greedy -> env.step -> replay.push
+//   simulator.py:59-93         kNN graph -> argmax -> env.step -> metrics
+//   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:242-321
+#include "swarm_tile.h"
+
+namespace swarm {
+
+enum { MODE_Q = 0, MODE_TICK = 1, MODE_ROLLOUT = 2, MODE_STEP = 3 };
+
+struct ActArgs {
+  int B, N, scenario, graph, k, conv, env_offset, flags;
+  uint32_t k0, k1;
+  const float* params;
+  const float* x;          // MODE_Q node features [B*N][7]
+  const uint8_t* dense;    // SWARM_GRAPH_DENSE multiplicity
+  const int32_t* actions;  // MODE_STEP actions [B][N]
+  float* state;            // [B][N][4]
+  swarm_replay replay;     // replay.s == nullptr -> no push
+  const swarm_ctrl* ctrl;  // MODE_TICK: tick / eps / write_slot
+  swarm_act_out out;
+  int n_ticks;
+  uint32_t tick0;
+  float eps;
+};
+
+template <int NMAX, int MODE>
+__global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
+  __shared__ WaveLds L;
+  const Geom g = make_geom(blockIdx.x, A.N, A.B);
+  const int N = A.N;
+  const float* __restrict__ P = A.params;
+  const size_t node = g.valid ? (size_t)g.env * N + g.agent : 0;
+
+  FwdState F;
+  float px = 0.f, py = 0.f, vx = 0.f, vy = 0.f;
+  if (MODE == MODE_Q) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) F.x[k] = (g.valid && k < kFeat) ? A.x[node * kFeat + k] : 0.0f;
+    px = F.x[0]; py = F.x[1];
+  } else if (g.valid) {
+    const float4 st = *reinterpret_cast<const float4*>(A.state + node * 4);
+    px = st.x; py = st.y; vx = st.z; vy = st.w;
+  }
+
+  uint32_t tick = A.tick0;
+  float eps = A.eps;
+  uint32_t slot = 0;
+  if (MODE == MODE_TICK) {
+    tick = A.ctrl->tick;
+    eps = A.ctrl->eps;
+    slot = A.ctrl->write_slot;
+  }
+  const int n_ticks = (MODE == MODE_ROLLOUT) ? A.n_ticks : 1;
+  float rew_sum = 0.0f, hits_sum = 0.0f;
+
+  for (int it = 0; it < n_ticks; ++it) {
+    if (MODE != MODE_Q) {
+      F.x[0] = px; F.x[1] = py; F.x[2] = vx; F.x[3] = vy;
+      F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)g.agent; F.x[7] = 0.0f;
+      if (!g.valid) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
+      }
+    }
+    if (g.h == 0) { L.px[g.v] = px; L.py[g.v] = py; }
+    __syncthreads();
+    int mult[NMAX];
+    float c[NMAX];
+    if (MODE != MODE_STEP) tile_forward<NMAX>(P, g, N, A.graph, A.k, A.conv, A.dense, L, F, mult, c);
+
+    if (MODE == MODE_Q) {
+      if (g.valid && g.h == 0) {
+#pragma unroll
+        for (int a = 0; a < kActions; ++a) A.out.q[node * kActions + a] = F.q[a];
+      }
+      return;
+    }
+
+    // ---- eps-greedy (train_gcn_dqn.py:164-167), one Philox coin per env and tick
+    const uint32_t tk = tick + (uint32_t)it;
+    const uint32_t genv = (uint32_t)(A.env_offset + (g.valid ? g.env : 0));
+    int action = (MODE == MODE_STEP) ? (g.valid ? A.actions[node] : 0) : argmax9(F.q);
+    if (MODE != MODE_STEP && eps > 0.0f) {
+      const float coin = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x);
+      if (coin < eps) {
+        const u32x4 w = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(g.agent >> 2), A.k0, A.k1);
+        const int j = g.agent & 3;
+        const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
+        action = uniform_int(word, kActions);
+      }
+    }
+
+    // ---- env.step (VMAS World.step + scenario reward)
+    const StepOut o = agent_step<NMAX>(A.scenario, N, g.agent, px, py, vx, vy, action,
+                                       [&](int u, float& ux, float& uy) { ux = L.px[g.base + u]; uy = L.py[g.base + u]; });
+    if (g.h == 0) { L.red[g.v] = o.dgoal; L.red2[g.v] = (o.dobs <= 0.2f) ? 1.0f : 0.0f; }
+    __syncthreads();
+    float rew;
+    float dsum = L.red[g.base];
+    float hsum = L.red2[g.base];
+    for (int j = 1; j < N; ++j) { dsum = dsum + L.red[g.base + j]; hsum = hsum + L.red2[g.base + j]; }
+    if (A.scenario == SWARM_GOTO) {
+      rew = -L.red[g.base];
+      for (int j = 1; j < N; ++j) rew = rew + (-L.red[g.base + j]);   // go_to_position_scenario.py:112-113
+    } else {
+      rew = oa_reward(o.dgoal, o.dobs);
+    }
+    const float avg = dsum / (float)N;
+    if (A.scenario == SWARM_GOTO) hsum = 0.0f;
+
+    if (g.valid && g.h == 0) {
+      if (MODE == MODE_TICK || MODE == MODE_STEP) {
+        if (MODE == MODE_TICK && A.out.q) {
+#pragma unroll
+          for (int a = 0; a < kActions; ++a) A.out.q[node * kActions + a] = F.q[a];
+        }
+        if (A.out.actions) A.out.actions[node] = action;
+        if (A.out.reward) A.out.reward[node] = rew;
+        if (MODE == MODE_TICK && A.replay.s) {
+          const size_t ri = ((size_t)slot * A.B + g.env) * N + g.agent;
+          reinterpret_cast<float4*>(A.replay.s)[ri] = make_float4(px, py, vx, vy);
+          reinterpret_cast<float4*>(A.replay.s_next)[ri] = make_float4(o.px, o.py, o.vx, o.vy);
+          A.replay.r[ri] = rew;
+          A.replay.a[ri] = (uint8_t)action;
+        }
+        if (MODE == MODE_TICK && A.out.mult && A.graph != SWARM_GRAPH_DENSE) {
+          for (int u = 0; u < N; ++u) A.out.mult[((size_t)g.env * N + u) * N + g.agent] = (uint8_t)mult[u];
+        }
+        if (g.agent == 0) {
+          if (A.out.avg_dist) A.out.avg_dist[g.env] = avg;
+          if (A.out.hits) A.out.hits[g.env] = hsum;
+        }
+      } else {  // MODE_ROLLOUT
+        if (A.out.traj_pos) {
+          const size_t ti = ((size_t)it * A.B + g.env) * N + g.agent;
+          reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o.px, o.py);
+        }
+        if (g.agent == 0) {
+          if (A.out.traj_dist) A.out.traj_dist[(size_t)it * A.B + g.env] = avg;
+          if (A.out.traj_hits) A.out.traj_hits[(size_t)it * A.B + g.env] = hsum;
+        }
+      }
+    }
+    rew_sum = rew_sum + rew;
+    hits_sum = hits_sum + hsum;
+    px = o.px; py = o.py; vx = o.vx; vy = o.vy;
+    if ((MODE == MODE_TICK || MODE == MODE_STEP) && g.valid && g.h == 0 && A.out.obs) {
+      float* ob = A.out.obs + node * 6;
+      ob[0] = px; ob[1] = py; ob[2] = vx; ob[3] = vy; ob[4] = kGoalX; ob[5] = kGoalY;
+    }
+    if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && g.valid && g.h == 0 && g.agent == 0) {
+      if (A.out.avg_dist) A.out.avg_dist[g.env] = avg;
+      if (A.out.hits) A.out.hits[g.env] = hits_sum;
+    }
+    __syncthreads();
+  }
+  if (g.valid && g.h == 0) {
+    reinterpret_cast<float4*>(A.state)[node] = make_float4(px, py, vx, vy);
+    if (MODE == MODE_ROLLOUT) {
+      if (A.out.reward) A.out.reward[node] = rew_sum;
+      if (A.out.obs) {
+        float* ob = A.out.obs + node * 6;
+        ob[0] = px; ob[1] = py; ob[2] = vx; ob[3] = vy; ob[4] = kGoalX; ob[5] = kGoalY;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- reset
+// reset_world_at + generate_grid; centre from Philox + Box-Muller (fp32 libm)
+__global__ void reset_kernel(int B, int N, int scenario, int flags, uint32_t k0, uint32_t k1, int env_offset,
+                             uint32_t episode, float* __restrict__ state) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = gid / N, agent = gid - env * N;
+  if (env >= B) return;
+  const uint32_t key_env = (flags & SWARM_F_SHARED_RESET) ? 0u : (uint32_t)(env_offset + env);
+  const u32x4 w = philox4x32(episode, key_env, STREAM_RESET, 0u, k0, k1);
+  const float u1 = ((float)(w.x >> 8) + 1.0f) * 5.9604644775390625e-08f;
+  const float u2 = (float)(w.y >> 8) * 5.9604644775390625e-08f;
+  const float rr = sqrtf(-2.0f * logf(u1));
+  const float z0 = rr * cosf(6.283185307179586f * u2), z1 = rr * sinf(6.283185307179586f * u2);
+  float cx, cy;
+  if (scenario == SWARM_GOTO) {
+    cx = 1.5f + (-0.6f + 0.4f * z0);
+    cy = -1.5f + (0.6f + 0.4f * z1);
+  } else {
+    const float s = (flags & SWARM_F_RANDOM_OA) ? 0.1f : 0.0f;
+    cx = 0.6f + s * z0;
+    cy = -0.6f + s * z1;
+  }
+  int cols = 1;
+  while (cols * cols < N) ++cols;
+  const int rows = (N + cols - 1) / cols;
+  const int i = agent / cols, j = agent - i * cols;
+  const float ox = (float)(((double)j - (double)(cols - 1) / 2.0) * 0.15);
+  const float oy = (float)(((double)i - (double)(rows - 1) / 2.0) * 0.15);
+  reinterpret_cast<float4*>(state)[gid] = make_float4(cx + ox, cy + oy, 0.0f, 0.0f);
+}
+
+// ---------------------------------------------------------------- graph build
+template <int NMAX>
+__global__ __launch_bounds__(64) void graph_kernel(ActArgs A, uint8_t* __restrict__ mult_out) {
+  __shared__ WaveLds L;
+  const Geom g = make_geom(blockIdx.x, A.N, A.B);
+  const int N = A.N;
+  const size_t node = g.valid ? (size_t)g.env * N + g.agent : 0;
+  if (g.h == 0) {
+    L.px[g.v] = g.valid ? A.x[node * kFeat + 0] : 0.0f;
+    L.py[g.v] = g.valid ? A.x[node * kFeat + 1] : 0.0f;
+  }
+  __syncthreads();
+  if (A.graph == SWARM_GRAPH_KNN) {
+    const uint32_t m = g.valid ? knn_row<NMAX>(g, N, A.k, L) : 0u;
+    if (g.h == 0) L.knn[g.v] = m;
+  }
+  __syncthreads();
+  int mult[NMAX];
+  graph_mult<NMAX>(g, N, A.graph, L, A.dense, mult);
+  if (g.valid && g.h == 0)
+    for (int u = 0; u < N; ++u) mult_out[((size_t)g.env * N + u) * N + g.agent] = (uint8_t)mult[u];
+}
+
+// ---------------------------------------------------------------- PyG edge list -> dense multiplicity
+// Batch.from_data_list of G graphs of N nodes each (train_gcn_dqn.py:45): node id = g*N + local.
+// Counts are packed 4 per 32-bit word and added with integer atomics (order independent).
+__global__ void edges_to_mult_kernel(const int64_t* __restrict__ ei, int64_t E, int G, int N,
+                                     uint32_t* __restrict__ words, int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  const int64_t s = ei[i], d = ei[E + i];
+  const int64_t nn = (int64_t)G * N;
+  if (s < 0 || d < 0 || s >= nn || d >= nn || s / N != d / N) { atomicOr(err, 1); return; }
+  const int64_t b = s / N;
+  const int64_t u = s - b * N, v = d - b * N;
+  const int64_t byte = (b * N + u) * N + v;
+  atomicAdd(&words[byte >> 2], 1u << (8 * (int)(byte & 3)));
+}
+
+}  // namespace swarm
+
+using namespace swarm;
+
+namespace {
+
+int check_cfg(const swarm_config* c) {
+  if (!c || c->n_envs < 0 || c->n_agents < 1 || c->n_agents > 32) return SWARM_E_BADARG;
+  if (c->scenario != SWARM_GOTO && c->scenario != SWARM_OBSTACLE_AVOIDANCE) return SWARM_E_BADARG;
+  if (c->graph < 0 || c->graph > 2 || (c->conv != SWARM_CONV_GAT && c->conv != SWARM_CONV_GCN)) return SWARM_E_BADARG;
+  if (c->graph == SWARM_GRAPH_KNN && (c->knn_k < 1 || c->knn_k > c->n_agents)) return SWARM_E_KNN_K;
+  return 0;
+}
+
+ActArgs make_args(const swarm_config* c) {
+  ActArgs a = {};
+  a.B = c->n_envs; a.N = c->n_agents; a.scenario = c->scenario; a.graph = c->graph;
+  a.k = c->knn_k; a.conv = c->conv; a.env_offset = c->env_offset; a.flags = c->flags;
+  a.k0 = (uint32_t)(c->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(c->seed >> 32);
+  return a;
+}
+
+int n_tiles(const swarm_config* c) {
+  const int E = kTile / c->n_agents;
+  return (c->n_envs + E - 1) / E;
+}
+
+template <int MODE>
+int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
+  if (tiles == 0) return 0;
+  if (a.N <= 8) hipLaunchKernelGGL((act_kernel<8, MODE>), dim3(tiles), dim3(64), 0, st, a);
+  else if (a.N <= 16) hipLaunchKernelGGL((act_kernel<16, MODE>), dim3(tiles), dim3(64), 0, st, a);
+  else hipLaunchKernelGGL((act_kernel<32, MODE>), dim3(tiles), dim3(64), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int swarm_abi_version(void) { return SWARM_ABI_VERSION; }
+int swarm_n_params(void) { return N_PARAMS; }
+const char* swarm_build_info(void) { return "libswarm_hip gfx950 (MFMA f32 32x32x2 tiles, wave64)"; }
+
+int swarm_env_reset(const swarm_config* cfg, float* state, uint32_t episode, void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  const int n = cfg->n_envs * cfg->n_agents;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(reset_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, cfg->n_envs,
+                     cfg->n_agents, cfg->scenario, cfg->flags, (uint32_t)(cfg->seed & 0xFFFFFFFFu),
+                     (uint32_t)(cfg->seed >> 32), cfg->env_offset, episode, state);
+  return (int)hipGetLastError();
+}
+
+int swarm_env_step(const swarm_config* cfg, float* state, const int32_t* actions, const swarm_act_out* out,
+                   void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  if (!actions) return SWARM_E_BADARG;
+  ActArgs a = make_args(cfg);
+  a.state = state; a.actions = actions;
+  if (out) { a.out = *out; a.out.q = nullptr; a.out.mult = nullptr; }
+  return launch_act<MODE_STEP>(a, n_tiles(cfg), (hipStream_t)stream);
+}
+
+int swarm_build_graph(const swarm_config* cfg, const float* x, uint8_t* mult, void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  if (cfg->graph == SWARM_GRAPH_DENSE) return SWARM_E_BADARG;
+  ActArgs a = make_args(cfg);
+  a.x = x;
+  const int tiles = n_tiles(cfg);
+  if (tiles == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (a.N <= 8) hipLaunchKernelGGL((graph_kernel<8>), dim3(tiles), dim3(64), 0, st, a, mult);
+  else if (a.N <= 16) hipLaunchKernelGGL((graph_kernel<16>), dim3(tiles), dim3(64), 0, st, a, mult);
+  else hipLaunchKernelGGL((graph_kernel<32>), dim3(tiles), dim3(64), 0, st, a, mult);
+  return (int)hipGetLastError();
+}
+
+int swarm_edges_to_mult(const int64_t* edge_index, int64_t n_edges, int32_t n_graphs, int32_t n_nodes,
+                        uint8_t* mult, int32_t* err, void* stream) {
+  if (!edge_index || !mult || !err || n_graphs < 0 || n_nodes < 1 || n_nodes > 32 || n_edges < 0) return SWARM_E_BADARG;
+  if ((reinterpret_cast<uintptr_t>(mult) & 3u) != 0) return SWARM_E_BADARG;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t bytes = ((size_t)n_graphs * n_nodes * n_nodes + 3) & ~(size_t)3;
+  if (hipError_t e = hipMemsetAsync(mult, 0, bytes, st)) return (int)e;
+  if (hipError_t e = hipMemsetAsync(err, 0, sizeof(int32_t), st)) return (int)e;
+  if (n_edges == 0) return 0;
+  hipLaunchKernelGGL(edges_to_mult_kernel, dim3((unsigned)((n_edges + 255) / 256)), dim3(256), 0, st, edge_index,
+                     n_edges, n_graphs, n_nodes, reinterpret_cast<uint32_t*>(mult), err);
+  return (int)hipGetLastError();
+}
+
+int swarm_q_forward(const swarm_config* cfg, const float* params, const float* x, const uint8_t* mult, float* q,
+                    void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  if (cfg->graph == SWARM_GRAPH_DENSE && !mult) return SWARM_E_BADARG;
+  ActArgs a = make_args(cfg);
+  a.params = params; a.x = x; a.dense = mult; a.out.q = q;
+  return launch_act<MODE_Q>(a, n_tiles(cfg), (hipStream_t)stream);
+}
+
+int swarm_act_step(const swarm_config* cfg, const float* params, float* state, const swarm_replay* replay,
+                   const swarm_ctrl* ctrl, const swarm_act_out* out, void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  if (!ctrl || cfg->graph == SWARM_GRAPH_DENSE) return SWARM_E_BADARG;
+  ActArgs a = make_args(cfg);
+  a.params = params; a.state = state; a.ctrl = ctrl;
+  if (replay) a.replay = *replay;
+  if (out) a.out = *out;
+  return launch_act<MODE_TICK>(a, n_tiles(cfg), (hipStream_t)stream);
+}
+
+int swarm_rollout(const swarm_config* cfg, const float* params, float* state, int32_t n_ticks, uint32_t tick0,
+                  float eps, const swarm_act_out* out, void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  if (n_ticks < 0 || cfg->graph == SWARM_GRAPH_DENSE) return SWARM_E_BADARG;
+  ActArgs a = make_args(cfg);
+  a.params = params; a.state = state; a.n_ticks = n_ticks; a.tick0 = tick0; a.eps = eps;
+  if (out) a.out = *out;
+  if (n_ticks == 0) return 0;
+  return launch_act<MODE_ROLLOUT>(a, n_tiles(cfg), (hipStream_t)stream);
+}
+
+int swarm_host_topk_set(const float* dist, int32_t n, int32_t k, uint8_t* selected) {
+  if (!dist || !selected || n < 1 || n > 32) return SWARM_E_BADARG;
+  if (k < 1 || k > n) return SWARM_E_KNN_K;
+  const uint32_t m = topk_smallest_mask<32>(dist, n, k);
+  for (int j = 0; j < n; ++j) selected[j] = (uint8_t)((m >> j) & 1u);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+// swarm_common.h — constants, parameter layout, Philox and MFMA helpers shared by
+// every kernel of libswarm_hip.so (gfx950 / CDNA4 only).
+//
+// Arithmetic restated from (paths relative to the reference checkout):
+//   VMAS 1.4.0 World.step / scenarios   -> SURVEY.md §8(a) rows a1-a6
+//   GCN / PyG GATConv                    -> src/training/train_gcn_dqn.py:50-70
+// Every translation unit is compiled with -ffp-contract=off: a*b+c stays two
+// roundings unless written as fmaf(), which is what the VMAS/PyTorch CPU path does.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/swarm_hip.h"
+
+namespace swarm {
+
+// ---------------------------------------------------------------- constants
+constexpr int kHidden = 32;
+constexpr int kFeat = 7;
+constexpr int kActions = 9;
+constexpr int kTile = 32;            // node slots per wave (MFMA 32x32x2 f32 M/N)
+
+constexpr float kGoalX = -0.8f, kGoalY = 0.8f;      // go_to_position_scenario.py:86
+constexpr float kObstX = -0.1f, kObstY = 0.1f;      // obstacle_avoidance_scenario.py:247
+constexpr float kRadius = 0.05f;                    // VMAS Sphere() default radius
+constexpr float kCollisionForce = 100.0f;           // VMAS World collision_force
+constexpr float kContactMargin = 0.001f;            // VMAS World contact_margin
+constexpr float kMinDist = 1e-6f;                   // VMAS _get_constraint_forces
+constexpr float kDt = 0.1f;                         // VMAS dt (substeps = 1)
+constexpr float kDragKeep = 0.75f;                  // 1 - drag(0.25)
+constexpr float kLeakySlope = 0.2f;                 // GATConv negative_slope
+
+// flat parameter layout == GCN.state_dict() order (see oracle PARAM_ORDER)
+constexpr int OFF_ATT_SRC = 0;       // [32]
+constexpr int OFF_ATT_DST = 32;      // [32]
+constexpr int OFF_BIAS = 64;         // [32]   conv1.bias
+constexpr int OFF_W = 96;            // [32][7] conv1.lin.weight
+constexpr int OFF_W1 = 320;          // [32][32]
+constexpr int OFF_B1 = 1344;         // [32]
+constexpr int OFF_W2 = 1376;         // [9][32]
+constexpr int OFF_B2 = 1664;         // [9]
+constexpr int N_PARAMS = 1673;
+static_assert(OFF_B2 + kActions == N_PARAMS, "param layout");
+
+// RNG stream ids (third Philox counter word); must match oracle/philox.py
+constexpr uint32_t STREAM_COIN = 1;
+constexpr uint32_t STREAM_RAND_ACTION = 2;
+constexpr uint32_t STREAM_RESET = 3;
+constexpr uint32_t STREAM_SAMPLE = 4;
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return {c0, c1, c2, c3};
+}
+
+__host__ __device__ inline float u01(uint32_t w) {   // [0,1), exact in fp32
+  return (float)(w >> 8) * 5.9604644775390625e-08f;
+}
+__host__ __device__ inline int uniform_int(uint32_t w, uint32_t n) {
+  return (int)(((uint64_t)w * n) >> 32);
+}
+
+// keyed pseudo-random permutation of [0, n) by a 4-round alternating Feistel
+// network on a 2^bits domain + cycle walking (oracle: sample_index).  Cycle walking
+// terminates because x lies on a permutation cycle that re-enters [0, n).
+__host__ __device__ inline uint32_t feistel(uint32_t x, int bits, uint32_t k0, uint32_t k1, uint32_t rnd) {
+  const int lo_bits = bits / 2, hi_bits = bits - lo_bits;
+  const uint32_t lo_mask = (1u << lo_bits) - 1u, hi_mask = (1u << hi_bits) - 1u;
+  uint32_t L = x >> lo_bits, R = x & lo_mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if ((r & 1) == 0) R ^= philox4x32(L, (uint32_t)r, STREAM_SAMPLE, rnd, k0, k1).x & lo_mask;
+    else              L ^= philox4x32(R, (uint32_t)r, STREAM_SAMPLE, rnd, k0, k1).x & hi_mask;
+  }
+  return (L << lo_bits) | R;
+}
+__host__ __device__ inline uint32_t sample_index(uint32_t i, uint32_t n, uint32_t k0, uint32_t k1, uint32_t rnd) {
+  int bits = 2;
+  while (bits < 32 && (1u << bits) < n) ++bits;
+  uint32_t x = i;
+  do { x = feistel(x, bits, k0, k1, rnd); } while (x >= n);
+  return x;
+}
+
+// ---------------------------------------------------------------- small math
+__host__ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * kLeakySlope; }
+
+// torch.linalg.vector_norm of a 2-vector on CPU == sqrtf(fmaf(dy, dy, dx*dx))
+// (re-checked by tests/test_knn_host.py against torch).
+__host__ __device__ inline float norm2(float dx, float dy) { return sqrtf(fmaf(dy, dy, dx * dx)); }
+
+// torch.logaddexp(0, x) CPU scalar path: max(0,x) + log1p(exp(-|x|))
+__device__ inline float logaddexp0(float x) {
+  const float m = x > 0.0f ? x : 0.0f;
+  return m + log1pf(expf(-fabsf(x)));
+}
+
+// VMAS _get_constraint_forces (attractive = False): force on entity a of the
+// pair (a, b) with delta = p_a - p_b; force on b is the exact negation.
+__device__ inline void pair_force(float dx, float dy, float& fx, float& fy) {
+  const float dist = norm2(dx, dy);
+  const float dmin = kRadius + kRadius;
+  const float pen = logaddexp0((dmin - dist) / kContactMargin) * kContactMargin;
+  const float den = dist > 0.0f ? dist : 1e-8f;
+  fx = kCollisionForce * dx / den * pen;
+  fy = kCollisionForce * dy / den * pen;
+  if (dist < kMinDist || dist > dmin) { fx = 0.0f; fy = 0.0f; }
+}
+
+// discrete action a in 0..8 -> u = (L[a/3], L[a%3]), L = {0, -1, +1}  
+__host__ __device__ inline float action_level(int l) { return l == 0 ? 0.0f : (l == 1 ? -1.0f : 1.0f); }
+
+// ---------------------------------------------------------------- MFMA (f32 in / f32 acc)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// D = A(32xK=2) * B(2x32) + C ; lane l supplies A[l&31][l>>5] and B[l>>5][l&31];
+// D element r of lane l is D[row=(r&3)+8(r>>2)+4(l>>5)][col=l&31].  Bit-exact k-ordered fmaf chain.
+__device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// row index of accumulator register r in lane half h ("acc layout")
+__host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ inline float xor32(float v) { return __shfl_xor(v, 32, 64); }
+
+}  // namespace swarm

@@ -1,0 +1,243 @@
+"""SwarmEngine: one rank's shard of vectorised swarm environments plus the DQN learner,
+all resident in HBM, driven through libswarm_hip.so.
+
+One training tick (the reference's hot loop, src/training/train_gcn_dqn.py:153-178):
+
+    swarm_act_step    graph -> GAT Q -> eps-greedy -> env.step -> replay push      (1 launch)
+    swarm_td_grad     sample -> target fwd -> online fwd -> TD loss -> backward      (1 launch)
+    swarm_grad_reduce deterministic slab sum                                         (1 launch)
+    [all_reduce(grad) over RCCL when world_size > 1]
+    swarm_adam_step   clip_grad_norm_ + Adam + target sync + ctrl advance            (1 launch)
+
+Every launch goes to torch's current stream, so a run of ticks can be captured
+once into a hipGraph (``capture``) and replayed.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import CTRL, N_PARAMS, SwarmActOut, SwarmAdamCfg, SwarmConfig, SwarmReplay, check, ptr, stream_ptr
+
+SCENARIOS = {"GoTo": _lib.SWARM_GOTO, "ObstacleAvoidance": _lib.SWARM_OBSTACLE_AVOIDANCE,
+             "go_to": _lib.SWARM_GOTO, "obstacle_avoidance": _lib.SWARM_OBSTACLE_AVOIDANCE}
+GRAPHS = {"complete": _lib.GRAPH_COMPLETE, "knn": _lib.GRAPH_KNN}
+CONVS = {"gat": _lib.CONV_GAT, "gcn": _lib.CONV_GCN}
+
+PARAM_ORDER = (
+    ("conv1.att_src", (1, 1, 32)), ("conv1.att_dst", (1, 1, 32)), ("conv1.bias", (32,)),
+    ("conv1.lin.weight", (32, 7)), ("lin1.weight", (32, 32)), ("lin1.bias", (32,)),
+    ("lin2.weight", (9, 32)), ("lin2.bias", (9,)),
+)
+
+
+def flatten_state_dict(sd, device=None) -> torch.Tensor:
+    return torch.cat([sd[k].detach().reshape(-1).to(torch.float32) for k, _ in PARAM_ORDER]).to(device)
+
+
+def unflatten_params(flat: torch.Tensor) -> dict:
+    out, o = {}, 0
+    for k, shape in PARAM_ORDER:
+        n = math.prod(shape)
+        out[k] = flat[o:o + n].reshape(shape).clone()
+        o += n
+    return out
+
+
+def glorot_init(generator: torch.Generator) -> torch.Tensor:
+    """Fresh GCN parameters: glorot for GATConv weights/attention (PyG reset_parameters),
+    torch.nn.Linear default init for lin1/lin2, zero GAT bias.  Init is not pinned by
+    any reference artefact; training runs normally start from it."""
+    def glorot(shape, fan_in, fan_out):
+        a = math.sqrt(6.0 / (fan_in + fan_out))
+        return (torch.rand(shape, generator=generator) * 2 - 1) * a
+
+    def linear(out_f, in_f):
+        b = 1.0 / math.sqrt(in_f)
+        w = (torch.rand(out_f, in_f, generator=generator) * 2 - 1) * b
+        bias = (torch.rand(out_f, generator=generator) * 2 - 1) * b
+        return w, bias
+
+    sd = {
+        "conv1.att_src": glorot((1, 1, 32), 1, 32),
+        "conv1.att_dst": glorot((1, 1, 32), 1, 32),
+        "conv1.bias": torch.zeros(32),
+        "conv1.lin.weight": glorot((32, 7), 7, 32),
+    }
+    sd["lin1.weight"], sd["lin1.bias"] = linear(32, 32)
+    sd["lin2.weight"], sd["lin2.bias"] = linear(9, 32)
+    return flatten_state_dict(sd)
+
+
+class SwarmEngine:
+    def __init__(self, scenario="GoTo", n_agents: int = 8, n_envs: int = 1024, *, seed: int = 0,
+                 graph: str = "complete", knn_k: int = 10, conv: str = "gat", params=None,
+                 batch: Optional[int] = None, gamma: float = 0.99, lr: float = 1e-3, betas=(0.9, 0.999),
+                 adam_eps: float = 1e-8, max_norm: float = 1.0, update_target_every: int = 200,
+                 replay_capacity: int = 1_000_000, env_offset: int = 0, world_size: int = 1,
+                 process_group=None, shared_reset: bool = False, random_oa: bool = True, eps: float = 0.05,
+                 device=None, learn: bool = True):
+        self.lib = _lib.load()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise RuntimeError("SwarmEngine runs on a ROCm GPU only (no CPU fallback)")
+        sid = SCENARIOS[scenario] if isinstance(scenario, str) else int(scenario)
+        flags = (_lib.F_SHARED_RESET if shared_reset else 0) | (_lib.F_RANDOM_OA if random_oa else 0)
+        self.cfg = SwarmConfig(n_envs, n_agents, sid, GRAPHS[graph], knn_k, CONVS[conv], env_offset, flags,
+                               seed & 0xFFFFFFFFFFFFFFFF)
+        self.B, self.N = n_envs, n_agents
+        self.scenario_id = sid
+        self.batch = n_envs if batch is None else batch
+        self.world_size = world_size
+        self.process_group = process_group
+        self.hp = SwarmAdamCfg(lr, betas[0], betas[1], adam_eps, max_norm, gamma, self.batch,
+                               update_target_every, world_size, 0)
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.state = torch.zeros(n_envs, n_agents, 4, **f32)
+        if params is None:
+            g = torch.Generator().manual_seed(seed)
+            params = glorot_init(g)
+        elif isinstance(params, dict):
+            params = flatten_state_dict(params)
+        self.params = params.detach().to(**f32).clone().contiguous()
+        assert self.params.numel() == N_PARAMS
+        self.target = self.params.clone()
+        self.adam_m = torch.zeros(N_PARAMS, **f32)
+        self.adam_v = torch.zeros(N_PARAMS, **f32)
+        self.ctrl = torch.zeros(_lib.CTRL_WORDS, dtype=torch.int32, device=dev)
+        self.set_eps(eps)
+        self.episode = 0
+        cap = max(1, -(-replay_capacity // n_envs)) if learn else 1
+        self.capacity = cap
+        self.rep_s = torch.zeros(cap, n_envs, n_agents, 4, **f32)
+        self.rep_s1 = torch.zeros(cap, n_envs, n_agents, 4, **f32)
+        self.rep_r = torch.zeros(cap, n_envs, n_agents, **f32)
+        self.rep_a = torch.zeros(cap, n_envs, n_agents, dtype=torch.uint8, device=dev)
+        self.replay = SwarmReplay(ptr(self.rep_s), ptr(self.rep_s1), ptr(self.rep_r), ptr(self.rep_a), cap, 0)
+        ws = self.lib.swarm_td_workspace_floats(ctypes_ref(self.cfg), self.batch)
+        if ws < 0:
+            check(int(ws), "swarm_td_workspace_floats")
+        self.slabs = torch.zeros(int(ws), **f32)
+        self.grad = torch.zeros(N_PARAMS + 1, **f32)
+        # per-tick outputs
+        self.q = torch.zeros(n_envs, n_agents, 9, **f32)
+        self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
+        self.reward = torch.zeros(n_envs, n_agents, **f32)
+        self.obs = torch.zeros(n_envs, n_agents, 6, **f32)
+        self.avg_dist = torch.zeros(n_envs, **f32)
+        self.hits = torch.zeros(n_envs, **f32)
+        self.out = SwarmActOut(ptr(self.q), ptr(self.actions), ptr(self.reward), ptr(self.obs),
+                               ptr(self.avg_dist), ptr(self.hits), 0, 0, 0, 0)
+        self.out_min = SwarmActOut(0, 0, ptr(self.reward), 0, ptr(self.avg_dist), ptr(self.hits), 0, 0, 0, 0)
+
+    # ------------------------------------------------------------------ control block
+    def set_eps(self, eps: float):
+        self.ctrl.view(torch.float32)[CTRL["eps"]].fill_(float(eps))
+
+    def read_ctrl(self) -> dict:
+        c = self.ctrl.cpu()
+        f = c.view(torch.float32)
+        return dict(tick=int(c[0]), write_slot=int(c[1]), filled_slots=int(c[2]), adam_step=int(c[3]),
+                    eps=float(f[4]), loss=float(f[5]), grad_norm=float(f[6]), trained=int(c[7]))
+
+    def replay_len(self) -> int:
+        """len(GraphReplayBuffer) in graphs (one graph = one env transition)."""
+        return self.read_ctrl()["filled_slots"] * self.B
+
+    # ------------------------------------------------------------------ env
+    def reset(self, episode: Optional[int] = None):
+        ep = self.episode if episode is None else episode
+        check(self.lib.swarm_env_reset(ctypes_ref(self.cfg), ptr(self.state), ep, stream_ptr()), "swarm_env_reset")
+        self.episode = ep + 1
+        return self.state
+
+    def env_step(self, actions: torch.Tensor, out: Optional[SwarmActOut] = None):
+        a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+        check(self.lib.swarm_env_step(ctypes_ref(self.cfg), ptr(self.state), ptr(a),
+                                      ctypes_ref(out or self.out), stream_ptr()), "swarm_env_step")
+
+    # ------------------------------------------------------------------ acting
+    def act(self, push: bool = True, full_out: bool = True):
+        check(self.lib.swarm_act_step(ctypes_ref(self.cfg), ptr(self.params), ptr(self.state),
+                                      ctypes_ref(self.replay) if push else None, ptr(self.ctrl),
+                                      ctypes_ref(self.out if full_out else self.out_min), stream_ptr()),
+              "swarm_act_step")
+
+    def advance(self):
+        check(self.lib.swarm_ctrl_advance(ctypes_ref(self.cfg), ctypes_ref(self.replay), ptr(self.ctrl),
+                                          stream_ptr()), "swarm_ctrl_advance")
+
+    def rollout(self, n_ticks: int, tick0: int = 0, eps: float = 0.0, traj: bool = False, params=None):
+        """Acting-only rollout in one launch.  Returns per-env sums (and per-tick
+        trajectories when traj=True)."""
+        dev = self.device
+        res = dict(reward=torch.zeros(self.B, self.N, device=dev), hits=torch.zeros(self.B, device=dev),
+                   avg_dist=torch.zeros(self.B, device=dev), obs=torch.zeros(self.B, self.N, 6, device=dev))
+        if traj:
+            res["traj_pos"] = torch.zeros(n_ticks, self.B, self.N, 2, device=dev)
+            res["traj_dist"] = torch.zeros(n_ticks, self.B, device=dev)
+            res["traj_hits"] = torch.zeros(n_ticks, self.B, device=dev)
+        out = SwarmActOut(0, 0, ptr(res["reward"]), ptr(res["obs"]), ptr(res["avg_dist"]), ptr(res["hits"]), 0,
+                          ptr(res.get("traj_pos")), ptr(res.get("traj_dist")), ptr(res.get("traj_hits")))
+        p = self.params if params is None else params
+        check(self.lib.swarm_rollout(ctypes_ref(self.cfg), ptr(p), ptr(self.state), n_ticks, tick0, eps,
+                                     ctypes_ref(out), stream_ptr()), "swarm_rollout")
+        return res
+
+    # ------------------------------------------------------------------ learning
+    def td_grad(self, sample_in: Optional[torch.Tensor] = None, sample_out: Optional[torch.Tensor] = None):
+        check(self.lib.swarm_td_grad(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.params), ptr(self.target),
+                                     ctypes_ref(self.replay), ptr(self.ctrl), ptr(sample_in), ptr(sample_out),
+                                     ptr(self.slabs), stream_ptr()), "swarm_td_grad")
+        check(self.lib.swarm_grad_reduce(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
+                                         ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
+
+    def allreduce_grad(self):
+        if self.world_size > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.process_group)
+
+    def adam(self):
+        check(self.lib.swarm_adam_step(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.params), ptr(self.target),
+                                       ptr(self.adam_m), ptr(self.adam_v), ptr(self.grad), self.capacity,
+                                       ptr(self.ctrl), stream_ptr()), "swarm_adam_step")
+
+    def td_update(self, sample_in=None, sample_out=None):
+        self.td_grad(sample_in, sample_out)
+        self.allreduce_grad()
+        self.adam()
+
+    def train_tick(self, full_out: bool = False):
+        self.act(push=True, full_out=full_out)
+        self.td_update()
+
+    # ------------------------------------------------------------------ hipGraph
+    def capture(self, n_ticks: int, fn=None):
+        """Capture n_ticks calls of ``fn`` (default train_tick) into one hipGraph."""
+        fn = fn or self.train_tick
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for _ in range(n_ticks):
+                    fn()
+        torch.cuda.current_stream().wait_stream(s)
+        return graph
+
+    # ------------------------------------------------------------------ weights
+    def state_dict(self) -> dict:
+        return unflatten_params(self.params.detach().cpu())
+
+    def load_state_dict(self, sd):
+        self.params.copy_(flatten_state_dict(sd).to(self.device))
+        self.target.copy_(self.params)
+
+
+def ctypes_ref(obj):
+    import ctypes
+    return None if obj is None else ctypes.byref(obj)

@@ -1,0 +1,179 @@
+/* swarm_hip.h — C ABI of libswarm_hip.so, the MI355X (gfx950) hot path of the
+ * swarm-RL inner loop of davidedomini/experiments-2025-acsos-marl-for-swarming-behaviors.
+ *
+ * Conventions:
+ *   - every buffer is caller-owned DEVICE memory, contiguous, fp32 / int32 / uint8;
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream);
+ *   - every entry point returns 0 on success, a positive hipError_t, or a
+ *     negative SWARM_E_* code; nothing throws across the ABI;
+ *   - no allocation, no host synchronisation inside any call: every call can be
+ *     captured into a hipGraph.
+ *
+ * Reference interfaces each entry point replaces are cited per function
+ * (paths relative to the reference checkout; VMAS 1.4.0 / PyG 2.5.3 are the
+ * reference's third-party dependencies, restated in SURVEY.md §8(a)).
+ */
+#ifndef SWARM_HIP_H
+#define SWARM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWARM_ABI_VERSION 1
+
+#define SWARM_E_BADARG (-1)    /* invalid shape / config */
+#define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
+#define SWARM_E_NOGPU (-3)
+
+enum swarm_scenario { SWARM_GOTO = 0, SWARM_OBSTACLE_AVOIDANCE = 1 };
+enum swarm_graph { SWARM_GRAPH_COMPLETE = 0, SWARM_GRAPH_KNN = 1, SWARM_GRAPH_DENSE = 2 };
+enum swarm_conv { SWARM_CONV_GAT = 0, SWARM_CONV_GCN = 1 };
+
+/* Static description of a batch of vectorised environments (one rank's shard). */
+typedef struct swarm_config {
+  int32_t n_envs;       /* B: environments handled by this call                         */
+  int32_t n_agents;     /* N: agents per environment, 1..32                             */
+  int32_t scenario;     /* swarm_scenario                                               */
+  int32_t graph;        /* swarm_graph: complete (train_gcn_dqn.py:101-108), kNN (simulator.py:15-24),
+                           or DENSE = caller-supplied multiplicity matrix [B][N][N] uint8  */
+  int32_t knn_k;        /* k of the kNN graph (reference code: 10, recorded data: 5)    */
+  int32_t conv;         /* swarm_conv: GAT (the reference's GCN class) or GCNConv (a13) */
+  int32_t env_offset;   /* global index of env 0 (rank sharding; keys the RNG)          */
+  int32_t flags;        /* SWARM_F_* bits                                               */
+  uint64_t seed;        /* Philox key                                                   */
+} swarm_config;
+
+#define SWARM_F_SHARED_RESET 1   /* one reset centre for all envs (go_to_position_scenario.py:88) */
+#define SWARM_F_RANDOM_OA 2      /* ObstacleAvoidance random=True (obstacle_avoidance_scenario.py:248) */
+
+/* Device-resident control block; kernels read and advance it so that a tick
+ * sequence can be replayed from a captured hipGraph.  Layout is ABI. */
+typedef struct swarm_ctrl {
+  uint32_t tick;          /* completed ticks (the reference's `ticks` is tick + 1 during a tick) */
+  uint32_t write_slot;    /* replay slot the next tick writes                               */
+  uint32_t filled_slots;  /* valid replay slots, <= capacity                                */
+  uint32_t adam_step;     /* optimizer steps taken                                          */
+  float eps;              /* exploration epsilon for the next tick                          */
+  float loss;             /* last TD loss (0 when the update was skipped)                   */
+  float grad_norm;        /* last pre-clip global gradient norm                             */
+  uint32_t trained;       /* 1 if the last TD step updated the weights                      */
+  uint32_t episode;       /* episode counter (reset RNG key)                                */
+  uint32_t pad[7];
+} swarm_ctrl;
+
+/* Replay ring (GraphReplayBuffer, train_gcn_dqn.py:25-48), SoA, per rank:
+ * slot t holds the B transitions pushed at one tick. Graph id g = slot*B + env. */
+typedef struct swarm_replay {
+  float* s;          /* [cap][B][N][4]  state before the tick: pos.xy, vel.xy */
+  float* s_next;     /* [cap][B][N][4]  state after the tick                 */
+  float* r;          /* [cap][B][N]     per-agent reward                     */
+  uint8_t* a;        /* [cap][B][N]     action                               */
+  int32_t capacity;  /* slots                                                */
+  int32_t pad;
+} swarm_replay;
+
+/* Per-tick outputs of the fused acting step; every pointer may be NULL. */
+typedef struct swarm_act_out {
+  float* q;          /* [B][N][9] Q-values                       */
+  int32_t* actions;  /* [B][N] chosen actions                    */
+  float* reward;     /* [B][N]                                   */
+  float* obs;        /* [B][N][6] pos, vel, goal after the step  */
+  float* avg_dist;   /* [B] scenario.average_distance_to_goal()  */
+  float* hits;       /* [B] scenario.obstacles_hits()            */
+  uint8_t* mult;     /* [B][N][N] edge multiplicity used         */
+  float* traj_pos;   /* rollout only: [T][B][N][2] positions after every tick */
+  float* traj_dist;  /* rollout only: [T][B] avg distance to goal per tick    */
+  float* traj_hits;  /* rollout only: [T][B] obstacle hits per tick          */
+} swarm_act_out;
+
+/* Optimizer hyper-parameters (train_gcn_dqn.py:85,112-137). */
+typedef struct swarm_adam_cfg {
+  float lr, beta1, beta2, eps;   /* Adam(lr=1e-3), torch defaults                 */
+  float max_norm;                /* clip_grad_norm_(…, 1)                          */
+  float gamma;                   /* 0.99                                           */
+  int32_t batch;                 /* sampled graphs per update (reference 32)       */
+  int32_t update_target_every;   /* 200 at train_gcn_dqn.py:175                   */
+  int32_t world_size;            /* ranks whose gradients are summed (grad /= W)   */
+  int32_t pad;
+} swarm_adam_cfg;
+
+int swarm_abi_version(void);
+int swarm_n_params(void);                 /* 1673 */
+const char* swarm_build_info(void);
+
+/* Reset: reset_world_at + generate_grid (go_to_position_scenario.py:52-106,
+ * obstacle_avoidance_scenario.py:63-133) for all B envs; state [B][N][4]. */
+int swarm_env_reset(const swarm_config* cfg, float* state, uint32_t episode, void* stream);
+
+/* VMAS Environment.step for discrete actions (call sites train_gcn_dqn.py:169,
+ * simulator.py:68): decode, holonomic force, sphere collisions, drag/Euler,
+ * scenario reward/observation/metrics.  actions [B][N] int32. */
+int swarm_env_step(const swarm_config* cfg, float* state, const int32_t* actions,
+                   const swarm_act_out* out, void* stream);
+
+/* Graph build: DQNTrainer.create_graph_from_observations (train_gcn_dqn.py:94-110)
+ * and simulator.create_graph_from_observations (simulator.py:9-26) as a dense
+ * per-env edge multiplicity mult[b][u][v] = #edges u->v.  pos from x[:, :2]. */
+int swarm_build_graph(const swarm_config* cfg, const float* x, uint8_t* mult, void* stream);
+
+/* PyG edge_index [2][E] int64 of a Batch of n_graphs graphs with n_nodes nodes each
+ * (Batch.from_data_list, train_gcn_dqn.py:45) -> dense multiplicity [G][N][N] uint8.
+ * mult must be 4-byte aligned with room for roundup4(G*N*N) bytes; *err (device
+ * int32) is set to 1 if an edge leaves its graph.  Multiplicities must stay < 256. */
+int swarm_edges_to_mult(const int64_t* edge_index, int64_t n_edges, int32_t n_graphs,
+                        int32_t n_nodes, uint8_t* mult, int32_t* err, void* stream);
+
+/* GCN.forward (train_gcn_dqn.py:59-70) on B per-env graphs of N nodes.
+ * x [B*N][7] node features; mult NULL unless cfg->graph == SWARM_GRAPH_DENSE. */
+int swarm_q_forward(const swarm_config* cfg, const float* params, const float* x,
+                    const uint8_t* mult, float* q, void* stream);
+
+/* Fused acting tick (train_gcn_dqn.py:161-172 / simulator.py:59-68):
+ * graph -> GAT Q -> eps-greedy (ctrl->eps, Philox) -> env.step -> replay push
+ * (replay may be NULL).  state updated in place. */
+int swarm_act_step(const swarm_config* cfg, const float* params, float* state,
+                   const swarm_replay* replay, const swarm_ctrl* ctrl,
+                   const swarm_act_out* out, void* stream);
+
+/* Acting-only rollout of n_ticks ticks with frozen weights in ONE launch
+ * (Simulator.run_simulation, simulator.py:59-93, greedy when eps = 0).
+ * out->reward / avg_dist / hits accumulate per-env sums over the ticks. */
+int swarm_rollout(const swarm_config* cfg, const float* params, float* state,
+                  int32_t n_ticks, uint32_t tick0, float eps, const swarm_act_out* out, void* stream);
+
+/* Workspace (floats) of swarm_td_grad's per-block gradient slabs. */
+int64_t swarm_td_workspace_floats(const swarm_config* cfg, int32_t batch);
+
+/* DQN TD-loss gradient (train_gcn_dqn.py:113-124): sample `batch` graphs from the
+ * replay (keyed Philox permutation; or sample_in [batch] graph ids if non-NULL),
+ * online forward, target forward + max, MSE, backward.  Writes per-block
+ * gradient slabs (+ loss partial in column N_PARAMS) to `slabs`.
+ * Skips (zero slabs, ctrl unchanged) while the replay holds < batch graphs. */
+int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* params,
+                  const float* target, const swarm_replay* replay, const swarm_ctrl* ctrl,
+                  const int32_t* sample_in, int32_t* sample_out, float* slabs, void* stream);
+
+/* Deterministic fixed-order sum of the slabs -> grad[N_PARAMS + 1] (last = loss sum). */
+int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
+                      float* grad, void* stream);
+
+/* clip_grad_norm_(1) + Adam step + target sync every `update_target_every` ticks,
+ * then advance ctrl (tick, replay slot).  grad is the (all-reduced) gradient sum. */
+int swarm_adam_step(const swarm_config* cfg, const swarm_adam_cfg* hp, float* params,
+                    float* target, float* adam_m, float* adam_v, const float* grad,
+                    int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
+
+/* Advance ctrl after an acting-only tick (no optimizer). */
+int swarm_ctrl_advance(const swarm_config* cfg, const swarm_replay* replay, swarm_ctrl* ctrl, void* stream);
+
+/* Host reference of the per-row neighbour selection the kernels run (CPU
+ * torch.topk(largest=False) set semantics, libstdc++ introselect); for tests. */
+int swarm_host_topk_set(const float* dist, int32_t n, int32_t k, uint8_t* selected);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWARM_HIP_H */

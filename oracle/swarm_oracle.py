@@ -1,0 +1,533 @@
+"""PyTorch-CPU fp32 restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+
+This module is the *checker* for the HIP path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it; the product path (``experiments-2025-acsos-marl-for-swarming-behaviors_amd``)
+never does and fails loudly when its HIP library is missing.
+
+What it restates (citations relative to the reference checkout):
+
+* VMAS 1.4.0 ``Environment.step`` for the two scenarios (third-party, not vendored;
+  ``requirements.txt:3``).  Arithmetic written out in SURVEY.md §8(a) rows a1-a6:
+  discrete decode, holonomic force, sphere-sphere collision force
+  (``World._sphere_sphere_vectorized_collision`` / ``_get_constraint_forces``),
+  drag + Euler integration, then the scenario ``reward`` / ``observation``.
+* ``GoToPositionScenario`` (``src/scenarios/go_to_position_scenario.py:52-143``).
+* ``ObstacleAvoidanceScenario`` (``src/scenarios/obstacle_avoidance_scenario.py:63-173``).
+* PyG 2.5.3 ``GATConv`` (heads=1, add_self_loops=False, negative_slope=0.2, bias)
+  and ``torch_geometric.utils.softmax`` (third-party, ``requirements.txt:2``).
+* ``GCN.forward`` (``src/training/train_gcn_dqn.py:59-70``).
+* Graph builders: training complete graph (``train_gcn_dqn.py:94-110``) and the
+  evaluation kNN graph (``src/simulation/simulator.py:9-26``).
+* ``DQNTrainer.train_step_dqn`` (``train_gcn_dqn.py:112-137``): gather, target max,
+  MSE, backward, ``clip_grad_norm_(…, 1)``, ``Adam(lr=1e-3)``.
+* ε-greedy (``train_gcn_dqn.py:161-169``) with the draws keyed through Philox
+  (``oracle/philox.py``) instead of Python ``random``.
+
+Parity pin: ``tests/test_oracle_golden.py`` checks this restatement against the
+reference's own recorded evaluation trajectories (``data/test_stats/**``) and
+trained weights (``data/models/*.pth``), committed as fixtures under
+``tests/golden/`` by ``tests/golden/make_golden.py``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import philox
+
+# ---------------------------------------------------------------------------
+# constants
+# ---------------------------------------------------------------------------
+GOAL = (-0.8, 0.8)              # go_to_position_scenario.py:86, obstacle_avoidance_scenario.py:245
+OBSTACLE = (-0.1, 0.1)          # obstacle_avoidance_scenario.py:247
+SPHERE_RADIUS = 0.05            # VMAS Sphere() default radius (agents and the obstacle)
+COLLISION_FORCE = 100.0         # VMAS World collision_force default
+CONTACT_MARGIN = 1e-3           # VMAS World contact_margin default
+MIN_DIST = 1e-6                 # VMAS _get_constraint_forces min_dist
+DT = 0.1                        # VMAS World dt, substeps=1
+DRAG = 0.25                     # VMAS World drag default
+GRID_SPACING = 0.15             # desired_distance (go_to_position_scenario.py:17)
+N_ACTIONS = 9
+N_FEATURES = 7
+HIDDEN = 32
+ACTION_LEVELS = (0.0, -1.0, 1.0)  # discrete level index -> u component
+
+SCENARIO_GOTO = 0
+SCENARIO_OA = 1
+
+PARAM_ORDER = (  # == GCN.parameters() order / state_dict order (PyG registers att, bias, then lin)
+    ("conv1.att_src", (1, 1, HIDDEN)),
+    ("conv1.att_dst", (1, 1, HIDDEN)),
+    ("conv1.bias", (HIDDEN,)),
+    ("conv1.lin.weight", (HIDDEN, N_FEATURES)),
+    ("lin1.weight", (HIDDEN, HIDDEN)),
+    ("lin1.bias", (HIDDEN,)),
+    ("lin2.weight", (N_ACTIONS, HIDDEN)),
+    ("lin2.bias", (N_ACTIONS,)),
+)
+N_PARAMS = sum(int(np.prod(s)) for _, s in PARAM_ORDER)  # 1673
+
+
+def f32(x):
+    return torch.as_tensor(x, dtype=torch.float32)
+
+
+# ---------------------------------------------------------------------------
+# parameters
+# ---------------------------------------------------------------------------
+def flatten_params(sd) -> torch.Tensor:
+    return torch.cat([sd[k].reshape(-1).to(torch.float32) for k, _ in PARAM_ORDER])
+
+
+def unflatten_params(flat) -> dict:
+    flat = torch.as_tensor(flat, dtype=torch.float32)
+    out, o = {}, 0
+    for k, shape in PARAM_ORDER:
+        n = int(np.prod(shape))
+        out[k] = flat[o:o + n].reshape(shape).clone()
+        o += n
+    return out
+
+
+# ---------------------------------------------------------------------------
+# env step  (VMAS World.step + scenario reward/observation)
+# ---------------------------------------------------------------------------
+def decode_actions(actions: torch.Tensor) -> torch.Tensor:
+    """a in 0..8 -> u = (L[a // 3], L[a % 3]), L = [0, -1, +1]."""
+    lv = torch.tensor(ACTION_LEVELS, dtype=torch.float32)
+    a = actions.to(torch.long)
+    return torch.stack([lv[a // 3], lv[a % 3]], dim=-1)
+
+
+def vector_norm2(d: torch.Tensor) -> torch.Tensor:
+    """torch.linalg.vector_norm over the last dim of size 2 (what VMAS/the scenarios call)."""
+    return torch.linalg.vector_norm(d, dim=-1)
+
+
+def pair_force(pos_a: torch.Tensor, pos_b: torch.Tensor, dist_min: float = 2 * SPHERE_RADIUS):
+    """VMAS _get_constraint_forces (attractive=False): force on a; force on b is its negation."""
+    delta = pos_a - pos_b
+    dist = vector_norm2(delta)
+    k = CONTACT_MARGIN
+    dmin = torch.full_like(dist, SPHERE_RADIUS) + torch.full_like(dist, SPHERE_RADIUS)
+    pen = torch.logaddexp(torch.tensor(0.0), (dmin - dist) * 1 / k) * k
+    force = COLLISION_FORCE * delta / torch.where(dist > 0, dist, torch.tensor(1e-8)).unsqueeze(-1) * pen.unsqueeze(-1)
+    force = torch.where((dist < MIN_DIST).unsqueeze(-1), torch.tensor(0.0), force)
+    force = torch.where((dist > dmin).unsqueeze(-1), torch.tensor(0.0), force)
+    return force
+
+
+def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenario: int):
+    """One VMAS step for [B, N] agents.  Returns dict of new state, rewards and metrics.
+
+    Force summation order follows VMAS: force = 0 + u, then the obstacle pair
+    (landmarks precede agents in ``world.entities``), then agent pairs (a<b) in
+    lexicographic order, i.e. ascending partner index for every agent.
+    """
+    pos = pos.to(torch.float32)
+    vel = vel.to(torch.float32)
+    B, N, _ = pos.shape
+    force = torch.zeros(B, N, 2) + decode_actions(actions)
+    obst = f32(OBSTACLE)
+    if scenario == SCENARIO_OA:
+        # pair (obstacle, agent_j): obstacle is entity_a -> agent receives -force_a
+        fa = pair_force(obst.expand(B, N, 2), pos)
+        force = force + (-fa)
+    for v in range(N):
+        acc = force[:, v]
+        for u in range(N):
+            if u == v:
+                continue
+            if u < v:   # pair (u, v): v is entity_b -> receives -force(p_u - p_v)
+                acc = acc + (-pair_force(pos[:, u], pos[:, v]))
+            else:       # pair (v, u): v is entity_a
+                acc = acc + pair_force(pos[:, v], pos[:, u])
+        force[:, v] = acc
+    vel_new = vel * (1 - DRAG)
+    accel = force / 1.0
+    vel_new = vel_new + accel * DT
+    pos_new = pos + vel_new * DT
+    goal = f32(GOAL)
+    dist_goal = vector_norm2(pos_new - goal)                    # [B, N]
+    if scenario == SCENARIO_GOTO:
+        r = torch.zeros(B)
+        acc = None
+        for j in range(N):                                      # go_to_position_scenario.py:108-115
+            acc = -dist_goal[:, j] if acc is None else acc + (-dist_goal[:, j])
+        rew = acc.unsqueeze(1).expand(B, N).clone()
+        d_obs = torch.zeros(B, N)
+        hits = torch.zeros(B)
+    else:
+        d_obs = (vector_norm2(pos_new - obst) - SPHERE_RADIUS) - SPHERE_RADIUS   # World.get_distance
+        obst_rew = torch.where(d_obs <= 1, -(1 - d_obs), torch.tensor(0.0))      # obstacle_avoidance_scenario.py:294-300
+        rew = -dist_goal + 2.5 * obst_rew
+        hits = (d_obs <= 0.2).sum(dim=1).to(torch.float32)                       # :318-321
+    avg_dist = torch.mean(dist_goal, dim=1)
+    return dict(pos=pos_new, vel=vel_new, force=force, rew=rew, dist_goal=dist_goal,
+                avg_dist=avg_dist, hits=hits, d_obs=d_obs)
+
+
+# ---------------------------------------------------------------------------
+# reset  (generate_grid + reset_world_at)
+# ---------------------------------------------------------------------------
+def grid_offsets(n_agents: int):
+    """go_to_position_scenario.py:52-80: row-major grid, cols = ceil(sqrt(N))."""
+    cols = math.ceil(math.sqrt(n_agents))
+    rows = math.ceil(n_agents / cols)
+    offs = []
+    for i in range(rows):
+        for j in range(cols):
+            offs.append(((j - (cols - 1) / 2) * GRID_SPACING, (i - (rows - 1) / 2) * GRID_SPACING))
+            if len(offs) >= n_agents:
+                break
+        if len(offs) >= n_agents:
+            break
+    return np.asarray(offs, dtype=np.float64)
+
+
+def grid_positions(centres: torch.Tensor, n_agents: int) -> torch.Tensor:
+    """centres [B,2] fp32 -> pos [B,N,2]; x = c + fp32(offset) (tensor + python float)."""
+    offs = torch.tensor(grid_offsets(n_agents), dtype=torch.float64).to(torch.float32)
+    return centres.to(torch.float32)[:, None, :] + offs[None, :, :]
+
+
+def reset_centres(scenario: int, n_envs: int, seed: int, episode: int, shared: bool, random_oa: bool = True):
+    """Reset centres with Philox + Box-Muller in float64 (the HIP reset kernel uses
+    fp32 libm calls, so reset positions are compared with a tolerance)."""
+    k0, k1 = philox.seed_key(seed)
+    envs = np.zeros(n_envs, dtype=np.uint32) if shared else np.arange(n_envs, dtype=np.uint32)
+    w = philox.philox4x32(np.uint32(episode), envs, philox.STREAM_RESET, 0, k0, k1)
+    u1 = ((w[0] >> np.uint32(8)).astype(np.float64) + 1.0) * 2.0 ** -24
+    u2 = (w[1] >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
+    rr = np.sqrt(-2.0 * np.log(u1))
+    z0, z1 = rr * np.cos(2 * np.pi * u2), rr * np.sin(2 * np.pi * u2)
+    if scenario == SCENARIO_GOTO:   # (1.5,-1.5) + N((-0.6,0.6), 0.4)
+        cx = np.float32(1.5) + (np.float32(-0.6) + np.float32(0.4) * z0.astype(np.float32))
+        cy = np.float32(-1.5) + (np.float32(0.6) + np.float32(0.4) * z1.astype(np.float32))
+    else:                           # (0.6,-0.6) + (random ? N(0,0.1) : 0)
+        s = np.float32(0.1) if random_oa else np.float32(0.0)
+        cx = np.float32(0.6) + s * z0.astype(np.float32)
+        cy = np.float32(-0.6) + s * z1.astype(np.float32)
+    return torch.tensor(np.stack([cx, cy], axis=1).astype(np.float32))
+
+
+# ---------------------------------------------------------------------------
+# observations / node features
+# ---------------------------------------------------------------------------
+def node_features(pos: torch.Tensor, vel: torch.Tensor) -> torch.Tensor:
+    """[B,N,7] = [pos, vel, goal, float(agent id)] (train_gcn_dqn.py:94-99)."""
+    B, N, _ = pos.shape
+    goal = f32(GOAL).expand(B, N, 2)
+    ids = torch.arange(N, dtype=torch.float32).view(1, N, 1).expand(B, N, 1)
+    return torch.cat([pos, vel, goal, ids], dim=-1)
+
+
+# ---------------------------------------------------------------------------
+# graph builders
+# ---------------------------------------------------------------------------
+def complete_edge_index(n: int) -> torch.Tensor:
+    """train_gcn_dqn.py:101-108: (i,j),(j,i) for i<j, then [0,0]."""
+    e = []
+    for i in range(n):
+        for j in range(i + 1, n):
+            e.append([i, j])
+            e.append([j, i])
+    e.append([0, 0])
+    return torch.tensor(e, dtype=torch.long).t().contiguous()
+
+
+def knn_edge_index(pos: torch.Tensor, k: int) -> torch.Tensor:
+    """simulator.py:15-24 for one env: pos [N,2] fp32."""
+    n = pos.shape[0]
+    e = []
+    for i in range(n):
+        d = torch.linalg.norm(pos[:, :2] - pos[i, :2], dim=1)
+        _, nearest = torch.topk(d, k, largest=False)
+        for a in nearest:
+            e.append([i, a.item()])
+            e.append([a.item(), i])
+    e.append([0, 0])
+    return torch.tensor(e, dtype=torch.long).t().contiguous()
+
+
+def knn_sets(pos: torch.Tensor, k: int) -> torch.Tensor:
+    """[B,N,2] -> bool [B, N(i), N(j)]: j in kNN(i), via the reference's own topk call."""
+    B, N, _ = pos.shape
+    out = torch.zeros(B, N, N, dtype=torch.bool)
+    for b in range(B):
+        for i in range(N):
+            d = torch.linalg.norm(pos[b, :, :2] - pos[b, i, :2], dim=1)
+            _, idx = torch.topk(d, k, largest=False)
+            out[b, i, idx] = True
+    return out
+
+
+def multiplicity_complete(B: int, N: int) -> torch.Tensor:
+    """m[b,u,v] = #edges u->v of the training graph."""
+    m = torch.ones(B, N, N) - torch.eye(N).expand(B, N, N)
+    m[:, 0, 0] = 1.0
+    return m
+
+
+def multiplicity_knn(sets: torch.Tensor) -> torch.Tensor:
+    """m(u->v) = [v in S_u] + [u in S_v] + [u=v=0]  (edges (i,j),(j,i) per j in S_i)."""
+    s = sets.to(torch.float32)
+    m = s + s.transpose(1, 2)
+    m[:, 0, 0] += 1.0
+    return m
+
+
+def edge_index_from_multiplicity(m: torch.Tensor) -> torch.Tensor:
+    """Batched multiplicity [B,N,N] -> PyG-style concatenated edge_index (duplicates expanded)."""
+    B, N, _ = m.shape
+    src, dst = [], []
+    for b in range(B):
+        for u in range(N):
+            for v in range(N):
+                for _ in range(int(m[b, u, v].item())):
+                    src.append(b * N + u)
+                    dst.append(b * N + v)
+    return torch.tensor([src, dst], dtype=torch.long)
+
+
+# ---------------------------------------------------------------------------
+# GAT / GCN forward
+# ---------------------------------------------------------------------------
+def gat_conv_edges(x, edge_index, W, att_src, att_dst, bias):
+    """PyG 2.5.3 GATConv(heads=1, add_self_loops=False) on an explicit edge list.
+
+    alpha_e = softmax_dst(leaky_relu(a_src[src] + a_dst[dst], 0.2)) with the
+    max taken over detached scores and a +1e-16 denominator; out = scatter_add
+    over dst of alpha * h[src]; + bias.
+    """
+    M = x.shape[0]
+    h = F.linear(x, W)                                           # lin (no bias)
+    a_s = (h * att_src.reshape(1, -1)).sum(-1)
+    a_d = (h * att_dst.reshape(1, -1)).sum(-1)
+    src, dst = edge_index[0], edge_index[1]
+    e = a_s[src] + a_d[dst]
+    e = F.leaky_relu(e, 0.2)
+    emax = torch.zeros(M, dtype=e.dtype).scatter_reduce(0, dst, e.detach(), reduce="amax", include_self=False)
+    ex = (e - emax[dst]).exp()
+    den = torch.zeros(M, dtype=e.dtype).scatter_add(0, dst, ex) + 1e-16
+    alpha = ex / den[dst]
+    msg = alpha.unsqueeze(-1) * h[src]
+    out = torch.zeros(M, h.shape[1], dtype=h.dtype).scatter_add(0, dst.unsqueeze(-1).expand_as(msg), msg)
+    return out + bias
+
+
+def q_forward_edges(params: dict, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+    """GCN.forward (train_gcn_dqn.py:59-70) on an edge list."""
+    g = gat_conv_edges(x, edge_index, params["conv1.lin.weight"], params["conv1.att_src"],
+                       params["conv1.att_dst"], params["conv1.bias"])
+    t = torch.tanh(g)
+    z = torch.relu(F.linear(t, params["lin1.weight"], params["lin1.bias"]))
+    return F.linear(z, params["lin2.weight"], params["lin2.bias"])
+
+
+def q_forward_dense(params: dict, x: torch.Tensor, mult: torch.Tensor, return_all: bool = False):
+    """Vectorised [B,N] restatement with a dense edge-multiplicity matrix mult[b,u,v].
+
+    Equals q_forward_edges on edge_index_from_multiplicity(mult) up to fp32
+    summation order (tests/test_oracle_internal.py checks it).
+    """
+    W = params["conv1.lin.weight"]
+    h = F.linear(x, W)                                           # [B,N,H]
+    a_s = (h * params["conv1.att_src"].reshape(1, 1, -1)).sum(-1)
+    a_d = (h * params["conv1.att_dst"].reshape(1, 1, -1)).sum(-1)
+    e = F.leaky_relu(a_s[:, :, None] + a_d[:, None, :], 0.2)     # [B,u,v]
+    present = mult > 0
+    neg = torch.tensor(float("-inf"))
+    emax = torch.where(present, e.detach(), neg).amax(dim=1)     # [B,v]
+    emax = torch.where(torch.isinf(emax), torch.zeros_like(emax), emax)
+    ex = torch.where(present, (e - emax[:, None, :]).exp(), torch.zeros_like(e))
+    den = (mult * ex).sum(dim=1) + 1e-16                         # [B,v]
+    alpha = ex / den[:, None, :]
+    out = torch.einsum("buv,buh->bvh", mult * alpha, h) + params["conv1.bias"]
+    t = torch.tanh(out)
+    z = torch.relu(F.linear(t, params["lin1.weight"], params["lin1.bias"]))
+    q = F.linear(z, params["lin2.weight"], params["lin2.bias"])
+    if return_all:
+        return dict(h=h, a_s=a_s, a_d=a_d, alpha=alpha, out=out, t=t, z=z, q=q)
+    return q
+
+
+def gcn_conv_dense(params: dict, x: torch.Tensor, mult: torch.Tensor):
+    """a13 (PARITY UNPINNED, not in the reference): PyG 2.5.3 GCNConv defaults on the
+    same multigraph: add_remaining_self_loops (self loops collapse to one weight-1
+    loop per node), deg counted on targets with duplicates, sym deg^-1/2 norm."""
+    W = params["conv1.lin.weight"]
+    h = F.linear(x, W)
+    B, N, _ = mult.shape
+    eye = torch.eye(N).expand(B, N, N)
+    # add_remaining_self_loops: existing (duplicate) self loops are dropped and one
+    # weight-1 loop per node is appended
+    m = mult * (1 - eye) + eye
+    deg = m.sum(dim=1)                                           # in-degree per target v
+    dis = deg.pow(-0.5)
+    dis = torch.where(torch.isinf(dis), torch.zeros_like(dis), dis)
+    norm = dis[:, :, None] * m * dis[:, None, :]
+    out = torch.einsum("buv,buh->bvh", norm, h) + params["conv1.bias"]
+    t = torch.tanh(out)
+    z = torch.relu(F.linear(t, params["lin1.weight"], params["lin1.bias"]))
+    return F.linear(z, params["lin2.weight"], params["lin2.bias"])
+
+
+def argmax_first(q: torch.Tensor) -> torch.Tensor:
+    """torch.argmax semantics (first maximal index)."""
+    return torch.argmax(q, dim=-1)
+
+
+# ---------------------------------------------------------------------------
+# ε-greedy with Philox draws
+# ---------------------------------------------------------------------------
+def egreedy(q: torch.Tensor, eps: float, seed: int, tick: int, env_offset: int = 0):
+    """One coin per env per tick; if coin < eps every agent draws uniform 0..8.
+
+    q: [B,N,9].  The reference draws one coin per tick for all agents of its
+    single env (train_gcn_dqn.py:164-167); the build keys it per env.
+    """
+    B, N, _ = q.shape
+    k0, k1 = philox.seed_key(seed)
+    envs = np.arange(B, dtype=np.uint32) + np.uint32(env_offset)
+    w = philox.philox4x32(np.uint32(tick), envs, philox.STREAM_COIN, 0, k0, k1)
+    coin = torch.tensor(philox.u01(w[0]))
+    explore = coin < torch.tensor(np.float32(eps))
+    rnd = torch.zeros(B, N, dtype=torch.long)
+    for g in range((N + 3) // 4):
+        wr = philox.philox4x32(np.uint32(tick), envs, philox.STREAM_RAND_ACTION, np.uint32(g), k0, k1)
+        for j in range(4):
+            i = 4 * g + j
+            if i < N:
+                rnd[:, i] = torch.tensor(philox.uniform_int(wr[j], N_ACTIONS))
+    greedy = argmax_first(q)
+    act = torch.where(explore[:, None], rnd, greedy)
+    return act, explore, greedy
+
+
+# ---------------------------------------------------------------------------
+# fused acting tick (graph -> GAT -> eps-greedy -> env step)
+# ---------------------------------------------------------------------------
+GRAPH_COMPLETE = 0
+GRAPH_KNN = 1
+
+
+@dataclass
+class TickOut:
+    q: torch.Tensor
+    actions: torch.Tensor
+    explore: torch.Tensor
+    greedy: torch.Tensor
+    step: dict
+    mult: torch.Tensor
+
+
+def act_tick(params: dict, pos, vel, scenario: int, graph: int, k: int, eps: float,
+             seed: int, tick: int, conv: str = "gat", env_offset: int = 0) -> TickOut:
+    B, N, _ = pos.shape
+    x = node_features(pos, vel)
+    if graph == GRAPH_COMPLETE:
+        mult = multiplicity_complete(B, N)
+    else:
+        mult = multiplicity_knn(knn_sets(pos, k))
+    if conv == "gat":
+        q = q_forward_dense(params, x, mult)
+    else:
+        q = gcn_conv_dense(params, x, mult)
+    act, explore, greedy = egreedy(q, eps, seed, tick, env_offset)
+    step = env_step(pos, vel, act, scenario)
+    return TickOut(q=q, actions=act, explore=explore, greedy=greedy, step=step, mult=mult)
+
+
+# ---------------------------------------------------------------------------
+# replay sampling (Feistel permutation; csrc swarm_sample_index)
+# ---------------------------------------------------------------------------
+def _feistel(x, bits, k0, k1, rnd):
+    """4-round alternating Feistel on (hi, lo) halves of a bits-wide word (bijective)."""
+    lo_bits = bits // 2
+    hi_bits = bits - lo_bits
+    lo_mask = (1 << lo_bits) - 1
+    hi_mask = (1 << hi_bits) - 1
+    L = x >> lo_bits
+    R = x & lo_mask
+    for r in range(4):
+        if r % 2 == 0:
+            w = philox.philox4x32(np.uint32(L), np.uint32(r), philox.STREAM_SAMPLE, np.uint32(rnd), k0, k1)[0]
+            R ^= int(w) & lo_mask
+        else:
+            w = philox.philox4x32(np.uint32(R), np.uint32(r), philox.STREAM_SAMPLE, np.uint32(rnd), k0, k1)[0]
+            L ^= int(w) & hi_mask
+    return (L << lo_bits) | R
+
+
+def sample_index(i: int, n: int, seed: int, rnd: int) -> int:
+    """i-th element of a keyed pseudo-random permutation of [0, n) (cycle walking)."""
+    bits = max(2, int(n - 1).bit_length())
+    k0, k1 = philox.seed_key(seed)
+    x = i
+    while True:
+        x = _feistel(x, bits, k0, k1, rnd)
+        if x < n:
+            return x
+
+
+# ---------------------------------------------------------------------------
+# TD step (train_gcn_dqn.py:112-137) with torch autograd / clip / Adam
+# ---------------------------------------------------------------------------
+def complete_batch_edge_index(S: int, N: int) -> torch.Tensor:
+    """Batch.from_data_list of S complete graphs (edge offsets by node count)."""
+    base = complete_edge_index(N)
+    return torch.cat([base + s * N for s in range(S)], dim=1)
+
+
+def td_step(flat_params, flat_target, adam_m, adam_v, adam_step: int,
+            s_state, actions, rewards, s_next_state, gamma=0.99, lr=1e-3,
+            betas=(0.9, 0.999), eps=1e-8, max_norm=1.0, edge_index=None, edge_index_next=None):
+    """One DQN update on S sampled graphs of N nodes.
+
+    s_state / s_next_state: [S,N,4] (pos, vel); actions [S,N] int; rewards [S,N].
+    Returns dict(loss, grad (pre-clip), total_norm, params, m, v, step).
+    """
+    S, N, _ = s_state.shape
+    params = {k: v.clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
+    tparams = unflatten_params(flat_target)
+    x = node_features(s_state[..., :2], s_state[..., 2:4]).reshape(S * N, N_FEATURES)
+    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4]).reshape(S * N, N_FEATURES)
+    ei = complete_batch_edge_index(S, N) if edge_index is None else edge_index
+    ein = ei if edge_index_next is None else edge_index_next
+    a = actions.reshape(-1).to(torch.long)
+    r = rewards.reshape(-1).to(torch.float32)
+    values = q_forward_edges(params, x, ei).gather(1, a.unsqueeze(1))
+    with torch.no_grad():
+        next_values = q_forward_edges(tparams, xn, ein).max(dim=1)[0]
+    target = r + gamma * next_values
+    loss = torch.nn.MSELoss()(values, target.unsqueeze(1))
+    plist = [params[k] for k, _ in PARAM_ORDER]
+    loss.backward()
+    grad = torch.cat([p.grad.reshape(-1) for p in plist]).clone()
+    total_norm = torch.nn.utils.clip_grad_norm_(plist, max_norm)
+    opt = torch.optim.Adam(plist, lr=lr, betas=betas, eps=eps, foreach=False)
+    if adam_step > 0:
+        st = opt.state_dict()
+        o = 0
+        for i, p in enumerate(plist):
+            n = p.numel()
+            st["state"][i] = {
+                "step": torch.tensor(float(adam_step)),
+                "exp_avg": torch.as_tensor(adam_m[o:o + n], dtype=torch.float32).reshape(p.shape).clone(),
+                "exp_avg_sq": torch.as_tensor(adam_v[o:o + n], dtype=torch.float32).reshape(p.shape).clone(),
+            }
+            o += n
+        opt.load_state_dict(st)
+    opt.step()
+    st = opt.state_dict()["state"]
+    m = torch.cat([st[i]["exp_avg"].reshape(-1) for i in range(len(plist))])
+    v = torch.cat([st[i]["exp_avg_sq"].reshape(-1) for i in range(len(plist))])
+    newp = torch.cat([p.detach().reshape(-1) for p in plist])
+    return dict(loss=float(loss.item()), grad=grad, total_norm=float(total_norm), params=newp,
+                m=m, v=v, step=adam_step + 1, values=values.detach().squeeze(1), target=target)

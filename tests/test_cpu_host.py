@@ -1,0 +1,162 @@
+"""CPU-only tests: library exports, neighbour-set semantics, oracle self-consistency,
+host-side API objects.  No GPU compute is called here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import knn_select, philox
+from oracle import swarm_oracle as O
+from tests.conftest import assert_close_rel
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _host_lib():
+    import swarm_amd._lib as L
+    if not os.path.exists(L.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return L, L.load(require_gpu=False)
+
+
+def test_library_exports_every_header_symbol():
+    L, lib = _host_lib()
+    hdr = open(os.path.join(ROOT, "include", "swarm_hip.h")).read()
+    names = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(swarm_\w+)\(", hdr, re.M))
+    assert len(names) >= 15
+    raw = ctypes.CDLL(L.LIB_PATH)
+    for n in sorted(names):
+        assert hasattr(raw, n), n
+    assert names == set(L.EXPORTED)
+    assert lib.swarm_abi_version() == 1 and lib.swarm_n_params() == O.N_PARAMS
+
+
+def test_topk_emulation_matches_torch_fixture():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "topk_ties.npz"))
+    for row, (n, k), s in zip(z["dist"], z["nk"], z["sets"]):
+        assert knn_select.topk_smallest_set(row[:n], int(k)) == sorted(np.where(s)[0].tolist())
+
+
+def test_host_topk_matches_torch_fixture():
+    """The C++ selection the kernels run (swarm_knn.h), compiled for the host."""
+    L, lib = _host_lib()
+    z = np.load(os.path.join(ROOT, "tests", "golden", "topk_ties.npz"))
+    sel = (ctypes.c_uint8 * 32)()
+    for row, (n, k), s in zip(z["dist"], z["nk"], z["sets"]):
+        d = np.ascontiguousarray(row[:n], dtype=np.float32)
+        rc = lib.swarm_host_topk_set(d.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(n), int(k), sel)
+        assert rc == 0
+        assert [j for j in range(n) if sel[j]] == sorted(np.where(s)[0].tolist())
+    assert lib.swarm_host_topk_set(np.zeros(4, np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                   4, 5, sel) == -2
+
+
+def test_host_topk_random_ties_vs_torch():
+    L, lib = _host_lib()
+    rng = np.random.default_rng(7)
+    sel = (ctypes.c_uint8 * 32)()
+    for _ in range(2000):
+        n = int(rng.integers(1, 33))
+        k = int(rng.integers(1, n + 1))
+        d = (rng.integers(0, 5, size=n).astype(np.float32) * np.float32(0.1)).astype(np.float32)
+        _, idx = torch.topk(torch.tensor(d), k, largest=False)
+        lib.swarm_host_topk_set(d.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, k, sel)
+        assert [j for j in range(n) if sel[j]] == sorted(idx.tolist())
+
+
+def test_philox_known_answers():
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff, 0xffffffff), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for c, k, e in kat:
+        assert tuple(int(x) for x in philox.philox4x32(*c, *k)) == e
+
+
+def test_sample_index_is_a_permutation():
+    for n in (1, 2, 3, 7, 64, 100, 1000):
+        got = sorted(O.sample_index(i, n, seed=5, rnd=3) for i in range(n))
+        assert got == list(range(n))
+
+
+@pytest.mark.parametrize("n", [1, 5, 8, 12])
+def test_dense_forward_equals_edge_list_forward(golden_weights, n):
+    params = O.unflatten_params(torch.tensor(golden_weights["go_to"][1]))
+    g = torch.Generator().manual_seed(n)
+    B = 6
+    pos = torch.randn(B, n, 2, generator=g) * 0.3
+    vel = torch.randn(B, n, 2, generator=g) * 0.1
+    x = O.node_features(pos, vel)
+    for mult in (O.multiplicity_complete(B, n), O.multiplicity_knn(O.knn_sets(pos, min(3, n)))):
+        qd = O.q_forward_dense(params, x, mult)
+        qe = O.q_forward_edges(params, x.reshape(B * n, 7), O.edge_index_from_multiplicity(mult))
+        assert_close_rel(qd.reshape(B * n, 9), qe, 1e-5, 'dense vs edge-list Q')
+
+
+def test_edge_builders_match_multiplicity():
+    pos = torch.tensor(O.grid_offsets(9), dtype=torch.float32)
+    ei = O.knn_edge_index(pos, 5)
+    m = O.multiplicity_knn(O.knn_sets(pos[None], 5))[0]
+    cnt = torch.zeros(9, 9)
+    for s, d in ei.t().tolist():
+        cnt[s, d] += 1
+    assert torch.equal(cnt, m)
+    ec = O.complete_edge_index(6)
+    cnt = torch.zeros(6, 6)
+    for s, d in ec.t().tolist():
+        cnt[s, d] += 1
+    assert torch.equal(cnt, O.multiplicity_complete(1, 6)[0])
+
+
+def test_td_step_oracle_reduces_loss(golden_weights):
+    """Sanity of the oracle learner itself: repeated updates on one batch lower the loss."""
+    p = torch.tensor(golden_weights["go_to"][2])
+    g = torch.Generator().manual_seed(0)
+    S, N = 4, 5
+    s = torch.randn(S, N, 4, generator=g) * 0.5
+    s1 = torch.randn(S, N, 4, generator=g) * 0.5
+    a = torch.randint(0, 9, (S, N), generator=g)
+    r = torch.randn(S, N, generator=g)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    losses = []
+    tgt = p.clone()
+    for step in range(30):
+        out = O.td_step(p, tgt, m, v, step, s, a, r, s1)
+        p, m, v = out["params"], out["m"], out["v"]
+        losses.append(out["loss"])
+    assert losses[-1] < losses[0]
+
+
+def test_gcn_module_state_dict_matches_reference_layout(golden_weights):
+    import swarm_amd
+    model = swarm_amd.GCN(7, 32, 9)
+    keys = list(model.state_dict().keys())
+    assert keys == [k for k, _ in O.PARAM_ORDER]
+    sd = O.unflatten_params(torch.tensor(golden_weights["obstacle_avoidance"][3]))
+    model.load_state_dict(sd)
+    assert torch.equal(model.flat_params("cpu"), torch.tensor(golden_weights["obstacle_avoidance"][3]))
+
+
+def test_graph_builders_host_side():
+    import swarm_amd
+    obs = {f"agent{i}": torch.randn(3, 6) for i in range(5)}
+    d = swarm_amd.create_graph_from_observations(obs)
+    assert d.x.shape == (15, 7) and d.swarm["n_graphs"] == 3
+    assert torch.equal(d.x.view(3, 5, 7)[..., 6], torch.arange(5.0).expand(3, 5))
+    with pytest.raises(RuntimeError):
+        swarm_amd.create_knn_graph_from_observations(obs, 5, k=10)
+    b = swarm_amd.Batch.from_data_list([d, d])
+    assert b.swarm["n_graphs"] == 6 and b.x.shape == (30, 7)
+
+
+def test_engine_refuses_cpu():
+    import swarm_amd
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        swarm_amd.SwarmEngine("GoTo", 8, 4)

@@ -1,0 +1,413 @@
+"""GPU parity: every HIP entry point vs the CPU oracle on identical seeded inputs.
+
+Bars (north_star): neighbour sets and multiplicities bit-exact; argmax equal
+wherever the oracle's top-2 Q gap exceeds 1e-4 (tie band); Q-values, TD loss,
+gradients within 1e-5 relative (``assert_close_rel``); physics within 1e-6.
+Also: the reference's recorded actions (tests/golden) reproduced on the GPU.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import swarm_oracle as O
+from tests.conftest import assert_close_rel
+
+pytestmark = pytest.mark.gpu
+
+SCEN = {"go_to": O.SCENARIO_GOTO, "obstacle_avoidance": O.SCENARIO_OA}
+
+
+@pytest.fixture(scope="module")
+def sw():
+    import swarm_amd
+    swarm_amd.load_library()
+    return swarm_amd
+
+
+def _params(golden_weights, scen="go_to", seed=0):
+    return torch.tensor(golden_weights[scen][seed])
+
+
+def _rand_state(B, N, seed, spread=0.12, tight=False):
+    g = torch.Generator().manual_seed(seed)
+    if tight:   # grid formations with small jitter: collisions and distance ties
+        off = torch.tensor(O.grid_offsets(N), dtype=torch.float32) * (0.5 if seed % 2 else 1.0)
+        c = torch.randn(B, 1, 2, generator=g)
+        pos = c + off[None] + (torch.randint(0, 3, (B, N, 2), generator=g).float() - 1) * 0.01
+    else:
+        pos = torch.randn(B, N, 2, generator=g) * spread * N ** 0.5
+    vel = torch.randn(B, N, 2, generator=g) * 0.2
+    return pos.float(), vel.float()
+
+
+def _tie_mask(q):
+    qs = q.sort(dim=-1, descending=True).values
+    return (qs[..., 0] - qs[..., 1]) > 1e-4
+
+
+# ------------------------------------------------------------------ env.step
+@pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
+@pytest.mark.parametrize("N", [1, 5, 8, 12, 29])
+def test_env_step_parity(sw, scen, N):
+    B = 96
+    eng = sw.SwarmEngine(scen, N, B, seed=1, learn=False)
+    for trial, tight in enumerate((False, True)):
+        pos, vel = _rand_state(B, N, 10 + trial, tight=tight)
+        acts = torch.randint(0, 9, (B, N), generator=torch.Generator().manual_seed(trial))
+        eng.state.copy_(torch.cat([pos, vel], -1).cuda())
+        eng.env_step(acts)
+        torch.cuda.synchronize()
+        ref = O.env_step(pos, vel, acts, SCEN[scen])
+        st = eng.state.cpu()
+        assert (st[..., 2:] - ref["vel"]).abs().max() <= 1e-6
+        assert (st[..., :2] - ref["pos"]).abs().max() <= 1e-6
+        assert_close_rel(eng.reward.cpu(), ref["rew"], 1e-6, "reward")
+        assert_close_rel(eng.avg_dist.cpu(), ref["avg_dist"], 1e-6, "avg_dist")
+        assert torch.equal(eng.hits.cpu(), ref["hits"])
+        assert torch.allclose(eng.obs.cpu()[..., :4], st, atol=0)
+        # agents with no neighbour within contact range: bit-exact physics
+        free = ref["force"].eq(O.decode_actions(acts)).all(-1)
+        assert torch.equal(st[..., :2][free], ref["pos"][free])
+
+
+# ------------------------------------------------------------------ reset
+@pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
+@pytest.mark.parametrize("shared", [True, False])
+def test_reset_parity(sw, scen, shared):
+    B, N = 50, 12
+    eng = sw.SwarmEngine(scen, N, B, seed=77, learn=False, shared_reset=shared, random_oa=True)
+    eng.reset(3)
+    torch.cuda.synchronize()
+    c = O.reset_centres(SCEN[scen], B, 77, 3, shared)
+    ref = O.grid_positions(c, N)
+    st = eng.state.cpu()
+    assert (st[..., :2] - ref).abs().max() < 2e-6
+    assert torch.equal(st[..., 2:], torch.zeros(B, N, 2))
+
+
+# ------------------------------------------------------------------ graph build
+@pytest.mark.parametrize("N,k", [(5, 5), (8, 5), (9, 5), (12, 10), (12, 5), (16, 7), (29, 10)])
+def test_knn_graph_bit_exact(sw, N, k):
+    import ctypes
+    from swarm_amd import _lib
+    B = 128
+    lib = _lib.load()
+    for tight in (True, False):
+        pos, vel = _rand_state(B, N, N * 31 + k, tight=tight)
+        x = O.node_features(pos, vel).reshape(B * N, 7)
+        mult = torch.zeros((B * N * N + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
+        cfg = _lib.SwarmConfig(B, N, 0, _lib.GRAPH_KNN, k, 0, 0, 0, 0)
+        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
+        got = mult[: B * N * N].view(B, N, N).cpu().float()
+        ref = O.multiplicity_knn(O.knn_sets(pos, k))
+        assert torch.equal(got, ref)
+        cfg.graph = _lib.GRAPH_COMPLETE
+        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
+        assert torch.equal(mult[: B * N * N].view(B, N, N).cpu().float(), O.multiplicity_complete(B, N))
+
+
+def test_knn_k_larger_than_n_raises(sw):
+    obs = {f"agent{i}": torch.randn(2, 6) for i in range(4)}
+    with pytest.raises(RuntimeError):
+        sw.create_knn_graph_from_observations(obs, 4, k=5)
+
+
+# ------------------------------------------------------------------ Q forward
+@pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
+@pytest.mark.parametrize("N", [1, 5, 8, 12, 20])
+@pytest.mark.parametrize("graph", ["complete", "knn"])
+def test_q_forward_parity(sw, golden_weights, scen, N, graph):
+    B = 100
+    model = sw.GCN(7, 32, 9)
+    model.load_state_dict(O.unflatten_params(_params(golden_weights, scen, N % 10)))
+    pos, vel = _rand_state(B, N, N)
+    obs = torch.cat([pos, vel, O.f32(O.GOAL).expand(B, N, 2)], -1)
+    k = min(5, N)
+    if graph == "complete":
+        data = sw.create_graph_from_observations(obs)
+        mult = O.multiplicity_complete(B, N)
+    else:
+        data = sw.create_knn_graph_from_observations(obs, N, k)
+        mult = O.multiplicity_knn(O.knn_sets(pos, k))
+    q = model(data).cpu().view(B, N, 9)
+    ref = O.q_forward_dense(O.unflatten_params(_params(golden_weights, scen, N % 10)), O.node_features(pos, vel), mult)
+    assert_close_rel(q, ref, 1e-5, "Q")
+    m = _tie_mask(ref)
+    assert torch.equal(q.argmax(-1)[m], ref.argmax(-1)[m])
+
+
+def test_q_forward_from_pyg_edge_index(sw, golden_weights):
+    """GCN.forward on a reference-style Data(x, edge_index) (Batch.from_data_list path)."""
+    N, G = 7, 5
+    params = _params(golden_weights, "go_to", 2)
+    model = sw.GCN(7, 32, 9)
+    model.load_state_dict(O.unflatten_params(params))
+    pos, vel = _rand_state(G, N, 3)
+    datas = []
+    for g in range(G):
+        x = O.node_features(pos[g:g + 1], vel[g:g + 1])[0]
+        datas.append(sw.Data(x=x, edge_index=O.knn_edge_index(pos[g], 4)))
+    batch = sw.Batch.from_data_list(datas)
+    q = model(batch).cpu()
+    ref = O.q_forward_edges(O.unflatten_params(params), batch.x, batch.edge_index)
+    assert_close_rel(q, ref, 1e-5, "Q(edge_index)")
+
+
+def test_gcn_variant_parity(sw, golden_weights):
+    B, N = 40, 9
+    p = _params(golden_weights, "obstacle_avoidance", 1)
+    model = sw.GCN(7, 32, 9, conv="gcn")
+    model.load_state_dict(O.unflatten_params(p))
+    pos, vel = _rand_state(B, N, 5)
+    obs = torch.cat([pos, vel, O.f32(O.GOAL).expand(B, N, 2)], -1)
+    q = model(sw.create_knn_graph_from_observations(obs, N, 4)).cpu().view(B, N, 9)
+    ref = O.gcn_conv_dense(O.unflatten_params(p), O.node_features(pos, vel), O.multiplicity_knn(O.knn_sets(pos, 4)))
+    assert_close_rel(q, ref, 1e-5, "GCN Q")
+
+
+# ------------------------------------------------------------------ recorded reference behaviour
+@pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
+def test_gpu_reproduces_recorded_reference_actions(sw, golden_weights, trajectories, scen):
+    total = match = 0
+    for seed in (0, 4):
+        model = sw.GCN(7, 32, 9)
+        model.load_state_dict(O.unflatten_params(_params(golden_weights, scen, seed)))
+        for n in (5, 8, 12):
+            xs, refs = [], []
+            for ep in range(8):
+                key = f"{scen}/s{seed}/n{n}/e{ep}"
+                P = trajectories[key + "/pos"]
+                P64 = P.astype(np.float64)
+                V = np.zeros_like(P64)
+                V[1:] = (P64[1:] - P64[:-1]) / 0.1
+                T = P.shape[0]
+                xs.append(O.node_features(torch.tensor(P[1:T - 1]), torch.tensor(V[1:T - 1].astype(np.float32))))
+                refs.append(torch.tensor(trajectories[key + "/ref_action"][1:T - 1].astype(np.int64)))
+            x = torch.cat(xs)                       # [G, n, 7]
+            ref = torch.cat(refs)
+            G = x.shape[0]
+            data = sw.Data(x.reshape(G * n, 7), None, swarm=dict(n_graphs=G, n_nodes=n, graph=1, k=5))
+            q = model(data).cpu().view(G, n, 9)
+            act = q.argmax(-1)
+            ok = act == ref
+            qs = q.sort(-1, descending=True).values
+            assert bool(((qs[..., 0] - qs[..., 1])[~ok] < 1e-4).all())
+            total += ok.numel()
+            match += int(ok.sum())
+    assert match / total >= 0.999
+
+
+# ------------------------------------------------------------------ fused acting tick
+@pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
+@pytest.mark.parametrize("N,graph,k", [(8, "complete", 0), (12, "knn", 10), (5, "knn", 5)])
+def test_act_tick_parity(sw, golden_weights, scen, N, graph, k):
+    B = 150
+    p = _params(golden_weights, scen, 7)
+    eng = sw.SwarmEngine(scen, N, B, seed=11, params=p, graph=graph, knn_k=max(k, 1), eps=0.35,
+                         replay_capacity=4 * B)
+    pos, vel = _rand_state(B, N, 21, tight=(N == 5))
+    eng.state.copy_(torch.cat([pos, vel], -1).cuda())
+    eng.ctrl[0] = 5   # tick
+    eng.act(push=True)
+    torch.cuda.synchronize()
+    ref = O.act_tick(O.unflatten_params(p), pos, vel, SCEN[scen], O.GRAPH_COMPLETE if graph == "complete" else O.GRAPH_KNN,
+                     k, 0.35, 11, 5)
+    assert_close_rel(eng.q.cpu(), ref.q, 1e-5, "Q")
+    clear = _tie_mask(ref.q) | ref.explore[:, None]
+    assert ref.explore.any() and (~ref.explore).any()
+    assert torch.equal(eng.actions.cpu().long()[clear], ref.actions[clear])
+    if clear.all():
+        assert (eng.state.cpu()[..., :2] - ref.step["pos"]).abs().max() <= 1e-6
+        assert_close_rel(eng.reward.cpu(), ref.step["rew"], 1e-6, "reward")
+        # replay push: slot 0 holds (s, a, r, s')
+        assert torch.equal(eng.rep_s[0].cpu(), torch.cat([pos, vel], -1))
+        assert torch.equal(eng.rep_a[0].cpu().long(), ref.actions)
+        assert torch.equal(eng.rep_s1[0].cpu(), eng.state.cpu())
+
+
+def test_rollout_equals_single_ticks(sw, golden_weights):
+    B, N, T = 64, 8, 12
+    p = _params(golden_weights, "go_to", 3)
+    a = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, graph="knn", knn_k=5, learn=False, eps=0.0)
+    b = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, graph="knn", knn_k=5, learn=False, eps=0.0)
+    a.reset(0)
+    b.reset(0)
+    rew = torch.zeros(B, N, device="cuda")
+    for t in range(T):
+        b.ctrl[0] = t
+        b.act(push=False)
+        rew += b.reward
+    r = a.rollout(T, tick0=0, eps=0.0, traj=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.state, b.state)
+    assert torch.allclose(r["reward"], rew, rtol=1e-6, atol=1e-5)
+    assert torch.equal(r["traj_pos"][-1], a.state[..., :2])
+
+
+# ------------------------------------------------------------------ learner
+def _fill_replay(eng, seed):
+    g = torch.Generator().manual_seed(seed)
+    cap, B, N = eng.rep_s.shape[:3]
+    eng.rep_s.copy_((torch.randn(cap, B, N, 4, generator=g) * 0.4).cuda())
+    eng.rep_s1.copy_((torch.randn(cap, B, N, 4, generator=g) * 0.4).cuda())
+    eng.rep_r.copy_(torch.randn(cap, B, N, generator=g).cuda())
+    eng.rep_a.copy_(torch.randint(0, 9, (cap, B, N), generator=g).to(torch.uint8).cuda())
+    eng.ctrl[2] = cap        # filled_slots
+    eng.ctrl[1] = 0
+
+
+@pytest.mark.parametrize("scen,N,S", [("go_to", 8, 32), ("obstacle_avoidance", 12, 40), ("go_to", 5, 7), ("go_to", 8, 256)])
+def test_td_update_parity(sw, golden_weights, scen, N, S):
+    B = 16
+    cap = max(4, -(-S // B))
+    p = _params(golden_weights, scen, 5)
+    tgt = _params(golden_weights, scen, 6)
+    eng = sw.SwarmEngine(scen, N, B, seed=2, params=p, batch=S, replay_capacity=cap * B, update_target_every=1000)
+    eng.target.copy_(tgt.cuda())
+    _fill_replay(eng, S)
+    idx = torch.randperm(cap * B, generator=torch.Generator().manual_seed(S))[:S].to(torch.int32)
+    eng.td_grad(sample_in=idx.cuda())
+    torch.cuda.synchronize()
+    slot, env = (idx // B).long(), (idx % B).long()
+    s = eng.rep_s.cpu()[slot, env]
+    s1 = eng.rep_s1.cpu()[slot, env]
+    a = eng.rep_a.cpu()[slot, env].long()
+    r = eng.rep_r.cpu()[slot, env]
+    ref = O.td_step(p, tgt, torch.zeros_like(p), torch.zeros_like(p), 0, s, a, r, s1)
+    grad = eng.grad.cpu()
+    loss = grad[O.N_PARAMS].item() / (S * N)
+    assert_close_rel(loss, ref["loss"], 1e-5, "TD loss")
+    gscale = ref["grad"].abs().max().clamp_min(1e-3)
+    assert ((grad[:O.N_PARAMS] - ref["grad"]).abs().max() / gscale).item() < 2e-5, "gradient"
+    eng.adam()
+    torch.cuda.synchronize()
+    c = eng.read_ctrl()
+    assert c["trained"] == 1 and c["adam_step"] == 1
+    assert abs(c["grad_norm"] - ref["total_norm"]) <= 1e-5 * max(1.0, ref["total_norm"])
+    assert (eng.params.cpu() - ref["params"]).abs().max().item() < 2e-6
+    assert_close_rel(eng.adam_v.cpu(), ref["v"], 1e-4, "adam v")
+
+
+def test_td_multi_step_adam_parity(sw, golden_weights):
+    """Three consecutive updates (bias corrections, state carry-over) vs the torch optimizer."""
+    B, N, S, cap = 8, 6, 24, 3
+    p = _params(golden_weights, "go_to", 8)
+    eng = sw.SwarmEngine("GoTo", N, B, seed=9, params=p, batch=S, replay_capacity=cap * B, update_target_every=2)
+    _fill_replay(eng, 99)
+    rp, rt = p.clone(), p.clone()
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for step in range(3):
+        idx = torch.randperm(cap * B, generator=torch.Generator().manual_seed(step))[:S].to(torch.int32)
+        eng.ctrl[0] = step      # tick -> (tick+1) % 2 == 0 syncs the target after step 1
+        eng.ctrl[2] = cap
+        eng.td_grad(sample_in=idx.cuda())
+        eng.adam()
+        slot, env = (idx // B).long(), (idx % B).long()
+        ref = O.td_step(rp, rt, m, v, step, eng.rep_s.cpu()[slot, env], eng.rep_a.cpu()[slot, env].long(),
+                        eng.rep_r.cpu()[slot, env], eng.rep_s1.cpu()[slot, env])
+        rp, m, v = ref["params"], ref["m"], ref["v"]
+        if (step + 1) % 2 == 0:
+            rt = rp.clone()
+    torch.cuda.synchronize()
+    assert (eng.params.cpu() - rp).abs().max().item() < 5e-6
+    assert (eng.target.cpu() - rt).abs().max().item() < 5e-6
+
+
+def test_replay_sampling_matches_oracle_and_is_distinct(sw):
+    B, N, S = 32, 4, 100
+    eng = sw.SwarmEngine("GoTo", N, B, seed=123, batch=S, replay_capacity=10 * B)
+    eng.ctrl[2] = 6          # filled slots -> 7 valid slots after this tick's push
+    eng.ctrl[0] = 17
+    out = torch.full((S,), -1, dtype=torch.int32, device="cuda")
+    eng.td_grad(sample_out=out)
+    got = out.cpu().tolist()
+    n = 7 * B
+    assert len(set(got)) == S and all(0 <= x < n for x in got)
+    k0 = 123 & 0xFFFFFFFF
+    ref = [O.sample_index(i, n, seed=k0, rnd=17) for i in range(S)]   # env_offset 0 -> key unchanged
+    assert got == ref
+
+
+def test_td_skips_until_replay_holds_a_batch(sw):
+    B, N = 8, 5
+    eng = sw.SwarmEngine("GoTo", N, B, seed=0, batch=32, replay_capacity=100 * B)
+    p0 = eng.params.clone()
+    eng.reset(0)
+    for t in range(3):             # 8, 16, 24 graphs < 32: skipped
+        eng.train_tick()
+        assert eng.read_ctrl()["trained"] == 0
+    assert torch.equal(eng.params, p0)
+    eng.train_tick()               # 32 graphs
+    c = eng.read_ctrl()
+    assert c["trained"] == 1 and c["tick"] == 4 and c["filled_slots"] == 4
+    assert not torch.equal(eng.params, p0)
+
+
+def test_training_is_bitwise_deterministic(sw, golden_weights):
+    p = _params(golden_weights, "obstacle_avoidance", 0)
+    outs = []
+    for _ in range(2):
+        eng = sw.SwarmEngine("ObstacleAvoidance", 8, 64, seed=5, params=p, batch=64, eps=0.3)
+        eng.reset(0)
+        for _ in range(6):
+            eng.train_tick()
+        torch.cuda.synchronize()
+        outs.append((eng.params.clone(), eng.state.clone(), eng.read_ctrl()["loss"]))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]) and outs[0][2] == outs[1][2]
+
+
+def test_graph_capture_replay_equals_eager(sw, golden_weights):
+    p = _params(golden_weights, "go_to", 1)
+    a = sw.SwarmEngine("GoTo", 8, 128, seed=8, params=p, batch=128, eps=0.1)
+    b = sw.SwarmEngine("GoTo", 8, 128, seed=8, params=p, batch=128, eps=0.1)
+    a.reset(0)
+    b.reset(0)
+    a.train_tick()
+    b.train_tick()
+    g = a.capture(5)
+    g.replay()
+    for _ in range(5):
+        b.train_tick()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params) and torch.equal(a.state, b.state)
+    assert a.read_ctrl() == b.read_ctrl()
+
+
+# ------------------------------------------------------------------ reference API drop-in
+def test_make_env_api_drop_in(sw):
+    env = sw.make_env(sw.GoToPositionScenario(), num_envs=1, device="cpu", continuous_actions=False, wrapper=None,
+                      max_steps=50, dict_spaces=True, seed=6967, n_agents=6, random=True, scenario_name="x")
+    obs = env.reset()
+    assert set(obs) == {f"agent{i}" for i in range(6)} and obs["agent0"].shape == (1, 6)
+    assert env.observation_space["agent0"].shape[0] == 6 and env.action_space["agent0"].n == 9
+    acts = {f"agent{i}": torch.tensor([i % 9]) for i in range(6)}
+    pos = torch.stack([obs[f"agent{i}"] for i in range(6)], 1).cpu()
+    obs2, rews, dones, infos = env.step(acts)
+    ref = O.env_step(pos[..., :2], pos[..., 2:4], torch.tensor([[i % 9 for i in range(6)]]), O.SCENARIO_GOTO)
+    assert torch.allclose(torch.stack([obs2[f"agent{i}"] for i in range(6)], 1).cpu()[..., :2], ref["pos"], atol=1e-6)
+    assert torch.allclose(rews["agent3"].cpu(), ref["rew"][:, 3], atol=1e-5)
+    assert float(env.scenario.average_distance_to_goal()) == pytest.approx(float(ref["avg_dist"][0]), abs=1e-5)
+    assert dones.shape == (1,) and not dones.any()
+
+
+def test_simulator_and_trainer_smoke(sw, golden_weights, tmp_path):
+    env = sw.make_env(sw.ObstacleAvoidanceScenario(), num_envs=1, continuous_actions=False, max_steps=20,
+                      dict_spaces=True, seed=1, n_agents=6, random=True)
+    model = sw.GCN(7, 32, 9)
+    model.load_state_dict(O.unflatten_params(_params(golden_weights, "obstacle_avoidance", 0)))
+    sim = sw.Simulator(env, model, 2, "obstacle_avoidance", 1, output_dir=str(tmp_path / "sim"), knn_k=5)
+    sim.run_simulation()
+    import csv
+    rows = list(csv.reader(open(tmp_path / "sim" / "result.csv")))
+    assert rows[0] == ["Episode", "Reward", "Collisions", "Distance (end)", "Distance (beginning)"] and len(rows) == 3
+    assert (tmp_path / "sim" / "positions" / "positions_episode_1_y.csv").exists()
+    env2 = sw.make_env(sw.GoToPositionScenario(), num_envs=4, continuous_actions=False, max_steps=10,
+                       dict_spaces=True, seed=0, n_agents=5)
+    tr = sw.DQNTrainer(env2, 0, str(tmp_path / "models"), str(tmp_path / "stats"), "GoTo", batch_size=8)
+    tr.train_model({"epsilon": 0.99, "epsilon_decay": 0.01, "min_epsilon": 0.05, "episodes": 10})
+    assert (tmp_path / "models" / "experiment_GoTo-seed_0.pth").exists()
+    sd = torch.load(tmp_path / "models" / "experiment_GoTo-seed_0.pth", weights_only=True)
+    assert list(sd.keys()) == [k for k, _ in O.PARAM_ORDER]
+    rows = list(csv.reader(open(tmp_path / "stats" / "experiment_GoTo-seed_0.csv")))
+    assert rows[0] == ["Episode", "Reward", "Loss"] and rows[1][0] == "9"

@@ -1,0 +1,93 @@
+"""Pin the CPU oracle to the reference's own recorded outputs (no GPU).
+
+Fixtures (tests/golden/, made by tests/golden/make_golden.py from
+/root/reference/data): trained weights and recorded evaluation trajectories of
+src/simulation/simulator.py (kNN k=5).  For every recorded tick the
+oracle rebuilds the observation (recorded positions + velocities derived from
+them), the kNN graph, the GAT Q-values and the argmax, and must reproduce the
+action the reference took (derived from the recorded next positions); it must
+also reproduce the recorded per-tick distance/hits and per-episode result.csv.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import swarm_oracle as O
+
+CASES = [(scen, sid, seed, n) for scen, sid in (("go_to", O.SCENARIO_GOTO), ("obstacle_avoidance", O.SCENARIO_OA))
+         for seed in (0, 4) for n in (5, 8, 12)]
+
+
+def _weights(golden_weights, scen, seed):
+    return O.unflatten_params(torch.tensor(golden_weights[scen][seed]))
+
+
+@pytest.mark.parametrize("scen,sid,seed,n", CASES)
+def test_oracle_reproduces_recorded_actions(golden_weights, trajectories, scen, sid, seed, n):
+    params = _weights(golden_weights, scen, seed)
+    total = match = 0
+    for ep in range(8):
+        key = f"{scen}/s{seed}/n{n}/e{ep}"
+        P = trajectories[key + "/pos"]                       # [T,N,2] fp32 recorded
+        ref = trajectories[key + "/ref_action"]
+        T = P.shape[0]
+        P64 = P.astype(np.float64)
+        V = np.zeros_like(P64)
+        V[1:] = (P64[1:] - P64[:-1]) / 0.1
+        pos = torch.tensor(P[1:T - 1])
+        vel = torch.tensor(V[1:T - 1].astype(np.float32))
+        x = O.node_features(pos, vel)
+        mult = O.multiplicity_knn(O.knn_sets(pos, 5))
+        q = O.q_forward_dense(params, x, mult)
+        act = O.argmax_first(q).numpy()
+        r = ref[1:T - 1]
+        ok = act == r
+        qs = q.sort(dim=-1, descending=True).values
+        gap = (qs[..., 0] - qs[..., 1]).numpy()
+        # misses allowed only at argmax near-ties (recorded velocities are derived, ~1e-6 noise)
+        assert np.all(gap[~ok] < 1e-4), f"{key}: clear-margin action mismatch"
+        total += ok.size
+        match += ok.sum()
+    assert match / total >= 0.999
+
+
+@pytest.mark.parametrize("scen,sid,seed,n", CASES)
+def test_oracle_env_step_matches_recorded_positions(trajectories, scen, sid, seed, n):
+    for ep in range(2):
+        key = f"{scen}/s{seed}/n{n}/e{ep}"
+        P = trajectories[key + "/pos"]
+        ref = trajectories[key + "/ref_action"]
+        P64 = P.astype(np.float64)
+        V = np.zeros_like(P64)
+        V[1:] = (P64[1:] - P64[:-1]) / 0.1
+        T = P.shape[0]
+        pos = torch.tensor(P[1:T - 1])
+        vel = torch.tensor(V[1:T - 1].astype(np.float32))
+        a = torch.tensor(ref[1:T - 1].astype(np.int64))
+        st = O.env_step(pos, vel, a, sid)
+        err = (st["pos"].double().numpy() - P64[2:T]).__abs__().max()
+        assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("scen,sid,seed,n", CASES)
+def test_oracle_metrics_match_recorded(trajectories, scen, sid, seed, n):
+    res = trajectories[f"{scen}/s{seed}/n{n}/result"]
+    for ep in range(8):
+        key = f"{scen}/s{seed}/n{n}/e{ep}"
+        P = torch.tensor(trajectories[key + "/pos"])
+        dist_goal = O.vector_norm2(P - O.f32(O.GOAL))                     # [T,N]
+        avg = torch.mean(dist_goal, dim=1).double().numpy()
+        np.testing.assert_allclose(avg, trajectories[key + "/dist"], atol=1e-6)
+        if sid == O.SCENARIO_OA:
+            d_obs = (O.vector_norm2(P - O.f32(O.OBSTACLE)) - O.SPHERE_RADIUS) - O.SPHERE_RADIUS
+            hits = (d_obs <= 0.2).sum(dim=1).double().numpy()
+            np.testing.assert_array_equal(hits, trajectories[key + "/hits"])
+            obst = torch.where(d_obs <= 1, -(1 - d_obs), torch.tensor(0.0))
+            rew = (-dist_goal + 2.5 * obst).sum(dim=1)
+        else:
+            rew = (-dist_goal).sum(dim=1) * P.shape[1]    # collective reward, identical for every agent
+        T = P.shape[0]
+        row = res[ep]
+        assert abs(rew.double().sum().item() / T - row[1]) <= 1e-4 * max(1.0, abs(row[1]))
+        assert abs(avg[-1] - row[3]) < 1e-6 and abs(avg[0] - row[4]) < 1e-6
+        assert trajectories[key + "/hits"].sum() == row[2]
