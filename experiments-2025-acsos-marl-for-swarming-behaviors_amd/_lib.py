@@ -13,7 +13,7 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_uint32, c_uint64, c_voi
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libswarm_hip.so")
+LIB_PATH = os.environ.get("SWARM_LIB_PATH") or os.path.join(HERE, "libswarm_hip.so")
 
 SWARM_GOTO, SWARM_OBSTACLE_AVOIDANCE = 0, 1
 GRAPH_COMPLETE, GRAPH_KNN, GRAPH_DENSE = 0, 1, 2
@@ -47,6 +47,10 @@ class SwarmAdamCfg(ctypes.Structure):
                 ("update_target_every", c_int32), ("world_size", c_int32), ("pad", c_int32)]
 
 
+class SwarmLearner(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("w_cur", "w_nxt", "m_cur", "m_nxt", "v_cur", "v_nxt", "target", "grad")]
+
+
 # swarm_ctrl is 16 x 4-byte words on the device; field -> word index
 CTRL_WORDS = 16
 CTRL = dict(tick=0, write_slot=1, filled_slots=2, adam_step=3, eps=4, loss=5, grad_norm=6, trained=7, episode=8)
@@ -62,6 +66,12 @@ _PROTOS = {
     "swarm_q_forward": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "swarm_act_step": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, POINTER(SwarmReplay), c_void_p,
                                  POINTER(SwarmActOut), c_void_p]),
+    "swarm_train_act_step": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
+                                       POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p]),
+    "swarm_reduce_advance": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p, POINTER(SwarmLearner),
+                                       c_int32, c_void_p, c_void_p]),
+    "swarm_adam_flush": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
+                                   c_void_p]),
     "swarm_rollout": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, c_int32, c_uint32, c_float,
                                 POINTER(SwarmActOut), c_void_p]),
     "swarm_td_workspace_floats": (c_int64, [POINTER(SwarmConfig), c_int32]),

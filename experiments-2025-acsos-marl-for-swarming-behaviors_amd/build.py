@@ -29,16 +29,22 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _deps())
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
-        return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+STAMPS_OUT = os.path.join(HERE, "libswarm_hip_stamps.so")
+
+
+def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> str:
+    """stamps=True builds the diagnostic library (in-kernel s_memtime stamps)."""
+    out = STAMPS_OUT if stamps else OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _deps()):
+        return out
+    extra = ["-DSWARM_STAMPS=1"] if stamps else []
+    cmd = [HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)

@@ -5,6 +5,7 @@
 //   train_gcn_dqn.py:161-172   graph -> model -> eps-greedy -> env.step -> replay.push
 //   simulator.py:59-93         kNN graph -> argmax -> env.step -> metrics
 //   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:242-321
+#include "swarm_adam.h"
 #include "swarm_tile.h"
 
 namespace swarm {
@@ -25,26 +26,66 @@ struct ActArgs {
   int n_ticks;
   uint32_t tick0;
   float eps;
+  int learn;               // MODE_TICK: apply the pending optimizer step first (fused tick)
+  swarm_learner lr;
+  swarm_adam_cfg hp;
+  float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
 };
 
+constexpr int kActTPB = 4;   // tiles (waves) per act block: weights staged / Adam applied once per 4 tiles
+
 template <int NMAX, int MODE>
-__global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
-  __shared__ WaveLds L;
-  const Geom g = make_geom(blockIdx.x, A.N, A.B);
+__global__ __launch_bounds__(64 * kActTPB) void act_kernel(ActArgs A) {
+  __shared__ WaveLds LW[kActTPB];
+  __shared__ __attribute__((aligned(16))) float Pw[N_PARAMS_PAD];
+  __shared__ float red[8 * kActTPB + 8];
+  SWARM_STAMP(0);
+  WaveLds& L = LW[threadIdx.x >> 6];
+  const Geom g = make_geom(blockIdx.x * kActTPB + (threadIdx.x >> 6), A.N, A.B);
   const int N = A.N;
-  const float* __restrict__ P = A.params;
   const size_t node = g.valid ? (size_t)g.env * N + g.agent : 0;
 
+  // prologue: every independent global load in flight at once
   FwdState F;
   float px = 0.f, py = 0.f, vx = 0.f, vy = 0.f;
   if (MODE == MODE_Q) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) F.x[k] = (g.valid && k < kFeat) ? A.x[node * kFeat + k] : 0.0f;
+    for (int k = 0; k < 8; ++k) F.x[k] = k < kFeat ? A.x[node * kFeat + k] : 0.0f;
+    if (!g.valid) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
+    }
     px = F.x[0]; py = F.x[1];
-  } else if (g.valid) {
+  } else {
     const float4 st = *reinterpret_cast<const float4*>(A.state + node * 4);
-    px = st.x; py = st.y; vx = st.z; vy = st.w;
+    if (g.valid) { px = st.x; py = st.y; vx = st.z; vy = st.w; }
   }
+  if (MODE == MODE_TICK && A.learn) {
+    // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
+    static_assert(64 * kActTPB == kAdamNT, "the act block is one Adam workgroup");
+    const int tid = threadIdx.x;
+    AdamRegs R;
+    R.load(A.lr.grad, A.lr.w_cur, A.lr.m_cur, A.lr.v_cur, tid);
+    const uint32_t pending = A.ctrl->trained;
+    const uint32_t tnow = A.ctrl->tick;
+    const double b1pow = ctrl_get_double(A.ctrl, CTRL_B1POW) * (double)A.hp.beta1;
+    const double b2pow = ctrl_get_double(A.ctrl, CTRL_B2POW) * (double)A.hp.beta2;
+    float gn = 0.0f;
+    if (pending) gn = adam_apply(R, A.hp, b1pow, b2pow, tid, red);
+    store_w_lds(Pw, R, tid);
+    if (blockIdx.x == 0) {
+      store4(A.lr.w_nxt, R.w, R.wt, tid);
+      store4(A.lr.m_nxt, R.m, R.mt, tid);
+      store4(A.lr.v_nxt, R.v, R.vt, tid);
+      if (pending && (tnow % (uint32_t)A.hp.update_target_every) == 0u) store4(A.lr.target, R.w, R.wt, tid);
+      if (pending && tid == 0) *A.grad_norm_out = gn;
+    }
+  } else if (MODE != MODE_STEP) {
+    ParamStage<64 * kActTPB> ps;
+    ps.load(A.params, threadIdx.x);
+    ps.store(Pw, threadIdx.x);
+  }
+  const float* P = Pw;
 
   uint32_t tick = A.tick0;
   float eps = A.eps;
@@ -68,9 +109,10 @@ __global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
     }
     if (g.h == 0) { L.px[g.v] = px; L.py[g.v] = py; }
     __syncthreads();
+    if (it == 0) SWARM_STAMP(1);
     int mult[NMAX];
     float c[NMAX];
-    if (MODE != MODE_STEP) tile_forward<NMAX>(P, g, N, A.graph, A.k, A.conv, A.dense, L, F, mult, c);
+    if (MODE != MODE_STEP) tile_forward<NMAX, 2>(P, g, N, A.graph, A.k, A.conv, A.dense, L, F, mult, c);
 
     if (MODE == MODE_Q) {
       if (g.valid && g.h == 0) {
@@ -86,7 +128,7 @@ __global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
     int action = (MODE == MODE_STEP) ? (g.valid ? A.actions[node] : 0) : argmax9(F.q);
     if (MODE != MODE_STEP && eps > 0.0f) {
       const float coin = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x);
-      if (coin < eps) {
+      if (coin < eps) {   // the action draw only runs on exploring envs
         const u32x4 w = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(g.agent >> 2), A.k0, A.k1);
         const int j = g.agent & 3;
         const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
@@ -94,23 +136,32 @@ __global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
       }
     }
 
+    if (it == 0) SWARM_STAMP(8);
     // ---- env.step (VMAS World.step + scenario reward)
     const StepOut o = agent_step<NMAX>(A.scenario, N, g.agent, px, py, vx, vy, action,
                                        [&](int u, float& ux, float& uy) { ux = L.px[g.base + u]; uy = L.py[g.base + u]; });
+    if (it == 0) SWARM_STAMP(9);
     if (g.h == 0) { L.red[g.v] = o.dgoal; L.red2[g.v] = (o.dobs <= 0.2f) ? 1.0f : 0.0f; }
     __syncthreads();
     float rew;
-    float dsum = L.red[g.base];
-    float hsum = L.red2[g.base];
-    for (int j = 1; j < N; ++j) { dsum = dsum + L.red[g.base + j]; hsum = hsum + L.red2[g.base + j]; }
+    float dj[NMAX], hj[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) { dj[j] = L.red[g.base + (j < N ? j : 0)]; hj[j] = L.red2[g.base + (j < N ? j : 0)]; }
+    float dsum = dj[0], hsum = hj[0];
+#pragma unroll
+    for (int j = 1; j < NMAX; ++j)
+      if (j < N) { dsum = dsum + dj[j]; hsum = hsum + hj[j]; }
     if (A.scenario == SWARM_GOTO) {
-      rew = -L.red[g.base];
-      for (int j = 1; j < N; ++j) rew = rew + (-L.red[g.base + j]);   // go_to_position_scenario.py:112-113
+      rew = -dj[0];
+#pragma unroll
+      for (int j = 1; j < NMAX; ++j)
+        if (j < N) rew = rew + (-dj[j]);   // go_to_position_scenario.py:112-113
     } else {
       rew = oa_reward(o.dgoal, o.dobs);
     }
     const float avg = dsum / (float)N;
     if (A.scenario == SWARM_GOTO) hsum = 0.0f;
+    if (it == 0) SWARM_STAMP(10);
 
     if (g.valid && g.h == 0) {
       if (MODE == MODE_TICK || MODE == MODE_STEP) {
@@ -157,6 +208,7 @@ __global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
       if (A.out.hits) A.out.hits[g.env] = hits_sum;
     }
     __syncthreads();
+    if (it == 0) SWARM_STAMP(11);
   }
   if (g.valid && g.h == 0) {
     reinterpret_cast<float4*>(A.state)[node] = make_float4(px, py, vx, vy);
@@ -168,6 +220,7 @@ __global__ __launch_bounds__(64) void act_kernel(ActArgs A) {
       }
     }
   }
+  SWARM_STAMP(12);
 }
 
 // ---------------------------------------------------------------- reset
@@ -270,9 +323,10 @@ int n_tiles(const swarm_config* c) {
 template <int MODE>
 int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   if (tiles == 0) return 0;
-  if (a.N <= 8) hipLaunchKernelGGL((act_kernel<8, MODE>), dim3(tiles), dim3(64), 0, st, a);
-  else if (a.N <= 16) hipLaunchKernelGGL((act_kernel<16, MODE>), dim3(tiles), dim3(64), 0, st, a);
-  else hipLaunchKernelGGL((act_kernel<32, MODE>), dim3(tiles), dim3(64), 0, st, a);
+  const dim3 grid((tiles + kActTPB - 1) / kActTPB), block(64 * kActTPB);
+  if (a.N <= 8) hipLaunchKernelGGL((act_kernel<8, MODE>), grid, block, 0, st, a);
+  else if (a.N <= 16) hipLaunchKernelGGL((act_kernel<16, MODE>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((act_kernel<32, MODE>), grid, block, 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -352,6 +406,19 @@ int swarm_act_step(const swarm_config* cfg, const float* params, float* state, c
   return launch_act<MODE_TICK>(a, n_tiles(cfg), (hipStream_t)stream);
 }
 
+int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
+                         const swarm_replay* replay, const swarm_ctrl* ctrl, const swarm_act_out* out, void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  if (!ctrl || !hp || !lr || cfg->graph == SWARM_GRAPH_DENSE || hp->world_size < 1 || hp->update_target_every < 1)
+    return SWARM_E_BADARG;
+  ActArgs a = make_args(cfg);
+  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp;
+  a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
+  if (replay) a.replay = *replay;
+  if (out) a.out = *out;
+  return launch_act<MODE_TICK>(a, n_tiles(cfg), (hipStream_t)stream);
+}
+
 int swarm_rollout(const swarm_config* cfg, const float* params, float* state, int32_t n_ticks, uint32_t tick0,
                   float eps, const swarm_act_out* out, void* stream) {
   if (int e = check_cfg(cfg)) return e;
@@ -362,6 +429,10 @@ int swarm_rollout(const swarm_config* cfg, const float* params, float* state, in
   if (n_ticks == 0) return 0;
   return launch_act<MODE_ROLLOUT>(a, n_tiles(cfg), (hipStream_t)stream);
 }
+
+#if SWARM_STAMPS
+int swarm_dbg_stamps_act(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_swarm_stamps), &p, sizeof(p)); }
+#endif
 
 int swarm_host_topk_set(const float* dist, int32_t n, int32_t k, uint8_t* selected) {
   if (!dist || !selected || n < 1 || n > 32) return SWARM_E_BADARG;

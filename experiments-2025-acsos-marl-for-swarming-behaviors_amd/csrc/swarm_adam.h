@@ -1,0 +1,150 @@
+// swarm_adam.h — clip_grad_norm_(max_norm) + Adam for the 1,673 GCN parameters,
+// executed by one workgroup of NT threads with everything in registers.  The same
+// code (same NT) runs in the fused act prologue (every block, redundantly, result
+// into its LDS weight image), in swarm_adam_flush and in the unfused
+// swarm_adam_step, so the three paths are bit-identical.
+//
+// Reference: train_gcn_dqn.py:125-126 (clip_grad_norm_(model.parameters(), 1);
+// Adam(lr=1e-3)).  torch semantics restated: per-tensor L2 norms, total = norm of
+// norms, coef = max_norm / (total + 1e-6) clamped to 1, grads *= coef; Adam
+// single_tensor: m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g g; denom = sqrt(v)/sqrt(bc2) + eps;
+// w += -(lr/bc1) * m/denom.  bc = 1 - beta^step with beta^step kept as a running
+// double product in the control block (python's beta ** step up to ~1e-16 relative).
+#pragma once
+#include "swarm_common.h"
+
+namespace swarm {
+
+constexpr int kAdamNT = 256;                           // threads of every Adam workgroup
+constexpr int kAdamNF4 = N_PARAMS / 4;                 // 418 float4 = floats 0..1671
+constexpr int kAdamNJ = (kAdamNF4 + kAdamNT - 1) / kAdamNT;
+static_assert(kAdamNF4 * 4 + 1 == N_PARAMS, "one tail element (lin2.bias[8])");
+
+// tensor index of float4 i (every tensor boundary is a multiple of 4 floats)
+__device__ inline int tensor_of_f4(int i) {
+  return i < OFF_ATT_DST / 4 ? 0 : i < OFF_BIAS / 4 ? 1 : i < OFF_W / 4 ? 2 : i < OFF_W1 / 4 ? 3
+       : i < OFF_B1 / 4 ? 4 : i < OFF_W2 / 4 ? 5 : i < OFF_B2 / 4 ? 6 : 7;
+}
+
+// beta^step running products live in the control block (doubles in the pad words)
+__device__ inline double ctrl_get_double(const swarm_ctrl* c, int word) {
+  const uint32_t* p = &c->beta_pow[word];
+  return __hiloint2double((int)p[1], (int)p[0]);
+}
+__device__ inline void ctrl_set_double(swarm_ctrl* c, int word, double v) {
+  c->beta_pow[word] = (uint32_t)__double2loint(v);
+  c->beta_pow[word + 1] = (uint32_t)__double2hiint(v);
+}
+constexpr int CTRL_B1POW = 0;   // beta_pow[0..1] = beta1^adam_step
+constexpr int CTRL_B2POW = 2;   // beta_pow[2..3] = beta2^adam_step
+
+struct AdamRegs {
+  float4 g[kAdamNJ], w[kAdamNJ], m[kAdamNJ], v[kAdamNJ];
+  float gt, wt, mt, vt;    // tail element N_PARAMS - 1
+
+  // every load issued unconditionally (clamped index): one memory round trip
+  __device__ inline void load(const float* __restrict__ grad, const float* __restrict__ w_, const float* __restrict__ m_,
+                              const float* __restrict__ v_, int tid) {
+#pragma unroll
+    for (int j = 0; j < kAdamNJ; ++j) {
+      const int i = min(tid + kAdamNT * j, kAdamNF4 - 1);
+      g[j] = reinterpret_cast<const float4*>(grad)[i];
+      w[j] = reinterpret_cast<const float4*>(w_)[i];
+      m[j] = reinterpret_cast<const float4*>(m_)[i];
+      v[j] = reinterpret_cast<const float4*>(v_)[i];
+    }
+    gt = grad[N_PARAMS - 1]; wt = w_[N_PARAMS - 1]; mt = m_[N_PARAMS - 1]; vt = v_[N_PARAMS - 1];
+  }
+};
+
+__device__ inline float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);
+  return x;
+}
+
+__device__ inline void adam_elem(float g, float& w, float& m, float& v, float one_m_b1, float beta2,
+                                 float one_m_b2, float bc2_sqrt, float eps, float step_size) {
+  m = m + one_m_b1 * (g - m);
+  v = v * beta2;
+  v = v + one_m_b2 * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  w = w + (-step_size) * (m / denom);
+}
+
+// One optimizer step in registers by the whole workgroup (kAdamNT threads; contains
+// __syncthreads).  b1pow/b2pow = beta^step for this (1-based) step.  Returns the
+// pre-clip global norm.  red: LDS scratch of >= 8 * (kAdamNT/64) + 8 floats.
+__device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, double b1pow, double b2pow, int tid,
+                                   float* red) {
+  const float inv_w = 1.0f / (float)hp.world_size;
+  float ss[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ss[k] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kAdamNJ; ++j) {
+    const int i = tid + kAdamNT * j;
+    float4 g = R.g[j];
+    if (hp.world_size > 1) { g.x = g.x * inv_w; g.y = g.y * inv_w; g.z = g.z * inv_w; g.w = g.w * inv_w; }
+    R.g[j] = g;
+    const float d = ((g.x * g.x + g.y * g.y) + g.z * g.z) + g.w * g.w;
+    const int t = i < kAdamNF4 ? tensor_of_f4(i) : -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ss[k] = ss[k] + (t == k ? d : 0.0f);
+  }
+  if (hp.world_size > 1) R.gt = R.gt * inv_w;
+  if (tid == 0) ss[7] = ss[7] + R.gt * R.gt;
+  constexpr int NW = kAdamNT / 64;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float s = wave_sum(ss[k]);
+    if ((tid & 63) == 0) red[k * NW + (tid >> 6)] = s;
+  }
+  __syncthreads();
+  float nn = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float s = red[k * NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) s = s + red[k * NW + w];
+    const float nk = sqrtf(s);
+    nn = nn + nk * nk;
+  }
+  const float total_norm = sqrtf(nn);
+  const float coef = hp.max_norm / (total_norm + 1e-6f);
+  const float clamped = coef < 1.0f ? coef : 1.0f;
+  const double bc1 = 1.0 - b1pow;
+  const double bc2 = 1.0 - b2pow;
+  const float step_size = (float)((double)hp.lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const float one_m_b1 = (float)(1.0 - (double)hp.beta1);
+  const float one_m_b2 = (float)(1.0 - (double)hp.beta2);
+#pragma unroll
+  for (int j = 0; j < kAdamNJ; ++j) {
+    float4 g = R.g[j], w = R.w[j], m = R.m[j], v = R.v[j];
+    adam_elem(g.x * clamped, w.x, m.x, v.x, one_m_b1, hp.beta2, one_m_b2, bc2_sqrt, hp.eps, step_size);
+    adam_elem(g.y * clamped, w.y, m.y, v.y, one_m_b1, hp.beta2, one_m_b2, bc2_sqrt, hp.eps, step_size);
+    adam_elem(g.z * clamped, w.z, m.z, v.z, one_m_b1, hp.beta2, one_m_b2, bc2_sqrt, hp.eps, step_size);
+    adam_elem(g.w * clamped, w.w, m.w, v.w, one_m_b1, hp.beta2, one_m_b2, bc2_sqrt, hp.eps, step_size);
+    R.w[j] = w; R.m[j] = m; R.v[j] = v;
+  }
+  adam_elem(R.gt * clamped, R.wt, R.mt, R.vt, one_m_b1, hp.beta2, one_m_b2, bc2_sqrt, hp.eps, step_size);
+  return total_norm;
+}
+
+__device__ inline void store4(float* __restrict__ dst, const float4* src, float tail, int tid) {
+#pragma unroll
+  for (int j = 0; j < kAdamNJ; ++j) {
+    const int i = tid + kAdamNT * j;
+    if (i < kAdamNF4) reinterpret_cast<float4*>(dst)[i] = src[j];
+  }
+  if (tid == 0) dst[N_PARAMS - 1] = tail;
+}
+
+// LDS weight image (N_PARAMS_PAD floats, pad zeroed)
+__device__ inline void store_w_lds(float* __restrict__ lds, const AdamRegs& R, int tid) {
+  store4(lds, R.w, R.wt, tid);
+  if (tid == 0) { lds[N_PARAMS] = 0.0f; lds[N_PARAMS + 1] = 0.0f; lds[N_PARAMS + 2] = 0.0f; }
+}
+
+}  // namespace swarm

@@ -40,6 +40,7 @@ constexpr int OFF_B1 = 1344;         // [32]
 constexpr int OFF_W2 = 1376;         // [9][32]
 constexpr int OFF_B2 = 1664;         // [9]
 constexpr int N_PARAMS = 1673;
+constexpr int N_PARAMS_PAD = 1676;   // 16-B multiple, LDS weight image
 static_assert(OFF_B2 + kActions == N_PARAMS, "param layout");
 
 // RNG stream ids (third Philox counter word); must match oracle/philox.py
@@ -73,30 +74,51 @@ __host__ __device__ inline int uniform_int(uint32_t w, uint32_t n) {
   return (int)(((uint64_t)w * n) >> 32);
 }
 
-// keyed pseudo-random permutation of [0, n) by a 4-round alternating Feistel
-// network on a 2^bits domain + cycle walking (oracle: sample_index).  Cycle walking
-// terminates because x lies on a permutation cycle that re-enters [0, n).
-__host__ __device__ inline uint32_t feistel(uint32_t x, int bits, uint32_t k0, uint32_t k1, uint32_t rnd) {
-  const int lo_bits = bits / 2, hi_bits = bits - lo_bits;
+// keyed pseudo-random permutation of [0, n): 4-round alternating Feistel network on a
+// 2^bits domain whose round function is the lowbias32 integer mixer keyed by one
+// Philox block (4 round keys), plus cycle walking (oracle: sample_index).  Cycle
+// walking terminates because x lies on a permutation cycle that re-enters [0, n).
+__host__ __device__ inline uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+struct SampleKey { uint32_t rk[4]; int bits; uint32_t n; };
+__host__ __device__ inline SampleKey sample_key(uint32_t n, uint32_t k0, uint32_t k1, uint32_t rnd) {
+  SampleKey s;
+  const u32x4 w = philox4x32(rnd, 0u, STREAM_SAMPLE, 0u, k0, k1);
+  s.rk[0] = w.x; s.rk[1] = w.y; s.rk[2] = w.z; s.rk[3] = w.w;
+  s.bits = 2;
+  while (s.bits < 32 && (1u << s.bits) < n) ++s.bits;
+  s.n = n;
+  return s;
+}
+__host__ __device__ inline uint32_t feistel(uint32_t x, const SampleKey& s) {
+  const int lo_bits = s.bits / 2, hi_bits = s.bits - lo_bits;
   const uint32_t lo_mask = (1u << lo_bits) - 1u, hi_mask = (1u << hi_bits) - 1u;
   uint32_t L = x >> lo_bits, R = x & lo_mask;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if ((r & 1) == 0) R ^= philox4x32(L, (uint32_t)r, STREAM_SAMPLE, rnd, k0, k1).x & lo_mask;
-    else              L ^= philox4x32(R, (uint32_t)r, STREAM_SAMPLE, rnd, k0, k1).x & hi_mask;
-  }
+  R ^= mix32(L ^ s.rk[0]) & lo_mask;
+  L ^= mix32(R ^ s.rk[1]) & hi_mask;
+  R ^= mix32(L ^ s.rk[2]) & lo_mask;
+  L ^= mix32(R ^ s.rk[3]) & hi_mask;
   return (L << lo_bits) | R;
 }
-__host__ __device__ inline uint32_t sample_index(uint32_t i, uint32_t n, uint32_t k0, uint32_t k1, uint32_t rnd) {
-  int bits = 2;
-  while (bits < 32 && (1u << bits) < n) ++bits;
+__host__ __device__ inline uint32_t sample_index(uint32_t i, const SampleKey& s) {
   uint32_t x = i;
-  do { x = feistel(x, bits, k0, k1, rnd); } while (x >= n);
+  do { x = feistel(x, s); } while (x >= s.n);
   return x;
 }
 
 // ---------------------------------------------------------------- small math
 __host__ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * kLeakySlope; }
+
+// tanh from one v_exp_f32 and one v_rcp_f32: t = sign(x) (1 - 2 / (exp(2|x|) + 1)).
+// |error| <= ~3e-7 absolute against torch.tanh (checked by the Q-value parity tests);
+// ocml tanhf costs ~230 cycles per call on the single-wave critical path.
+__device__ inline float tanh_fast(float x) {
+  const float e = __expf(2.0f * fabsf(x));
+  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+  return copysignf(t, x);
+}
 
 // torch.linalg.vector_norm of a 2-vector on CPU == sqrtf(fmaf(dy, dy, dx*dx))
 // (re-checked by tests/test_knn_host.py against torch).
@@ -110,14 +132,18 @@ __device__ inline float logaddexp0(float x) {
 
 // VMAS _get_constraint_forces (attractive = False): force on entity a of the
 // pair (a, b) with delta = p_a - p_b; force on b is the exact negation.
+// Pairs out of contact (dist > r_a + r_b) or coincident (dist < 1e-6) get exactly 0,
+// as the two torch.where of the reference do, so the transcendental part is skipped.
 __device__ inline void pair_force(float dx, float dy, float& fx, float& fy) {
   const float dist = norm2(dx, dy);
   const float dmin = kRadius + kRadius;
+  fx = 0.0f;
+  fy = 0.0f;
+  if (dist < kMinDist || dist > dmin) return;
   const float pen = logaddexp0((dmin - dist) / kContactMargin) * kContactMargin;
   const float den = dist > 0.0f ? dist : 1e-8f;
   fx = kCollisionForce * dx / den * pen;
   fy = kCollisionForce * dy / den * pen;
-  if (dist < kMinDist || dist > dmin) { fx = 0.0f; fy = 0.0f; }
 }
 
 // discrete action a in 0..8 -> u = (L[a/3], L[a%3]), L = {0, -1, +1}  
@@ -135,5 +161,29 @@ __device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
 __host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ inline float xor32(float v) { return __shfl_xor(v, 32, 64); }
+
+// ---------------------------------------------------------------- diagnostic stamps
+// Built only into the diagnostic library (-DSWARM_STAMPS=1, libswarm_hip_stamps.so):
+// lane 0 of every wave records s_memtime at named points; read their SHARES, never
+// the run time of that build (cdna_hip_programming.md §7 "In-kernel stamps").
+#ifndef SWARM_STAMPS
+#define SWARM_STAMPS 0
+#endif
+#if SWARM_STAMPS
+static __device__ unsigned long long* g_swarm_stamps;
+#define SWARM_STAMP(k)                                                                        \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long _t;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (g_swarm_stamps && (threadIdx.x & 63) == 0)                                            \
+      g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + (k)] = _t;         \
+  } while (0)
+#else
+#define SWARM_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 }  // namespace swarm

@@ -14,25 +14,35 @@
 //   (32x32x2 f32, node index as K), vectors by LDS column sums.
 // Each block writes one slab [N_PARAMS + 1] (last = sum of squared TD errors);
 // swarm_grad_reduce sums slabs in a fixed order (bitwise run-to-run reproducible).
+#include <stdlib.h>
+
+#include "swarm_adam.h"
 #include "swarm_tile.h"
 
 namespace swarm {
 
-struct TdLds {
-  WaveLds L;
-  float T[kTile][kHsStride];      // tanh(conv out), natural order
-  float R[kTile][kHsStride];      // relu(lin1)
-  float dZ[kTile][kHsStride];
+template <int NMAX>
+struct TdTileLds {
+  WaveLds L;                      // online forward scratch (H rows, scores, positions)
+  WaveLds LT;                     // target forward scratch
+  float T[kTile][kHsStride];      // tanh(conv out), natural order    } reused as this tile's
+  float R[kTile][kHsStride];      // relu(lin1)                        } partial slab after the
+  float dZ[kTile][kHsStride];     //                                   } parameter products
   float dO[kTile][kHsStride];     // dL/d conv out
   float dH[kTile][kHsStride];     // dL/d h
-  float X[kTile][kHsStride];      // features, cols >= 7 zero
-  float cm[kTile][kTile + 1];     // c[target slot][source agent]
-  float dp[kTile][kTile + 1];     // dp[target slot][source agent]
+  float X[kTile][9];              // features (k < 8)
+  float cm[kTile][NMAX + 1];      // c[target slot][source agent]
+  float dp[kTile][NMAX + 1];      // dp[target slot][source agent]
+  float y[kTile];                 // TD targets from the target wave
   float gq[kTile];
   float das[kTile], dad[kTile];
   float d2[kTile];
   int act[kTile];
 };
+static_assert(5 * kTile * kHsStride >= N_PARAMS + 1, "partial slab fits the image area");
+
+// tiles per block; each tile has an online wave and a target wave (2 * TPB waves)
+template <int NMAX> constexpr int td_tpb_max() { return NMAX <= 16 ? 3 : 2; }
 
 struct TdArgs {
   int S, B, N, graph, k, conv, env_offset;
@@ -63,126 +73,161 @@ __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kHsStride], const floa
   return acc;
 }
 
-template <int NMAX>
-__global__ __launch_bounds__(64) void td_kernel(TdArgs A) {
-  __shared__ TdLds T;
-  WaveLds& L = T.L;
+// Waves 0..TPB-1: online network of tile w (forward with activations kept, backward,
+// dW / att gradients); waves TPB..2TPB-1: target network of tile w-TPB (forward on s',
+// y = r + gamma max Q_tgt), then the dW1 / dW2 / bias products while the online wave
+// runs the GAT backward.  Every wave passes the same __syncthreads() sequence.
+template <int NMAX, int TPB>
+__global__ __launch_bounds__(128 * TPB) void td_kernel(TdArgs A) {
+  static_assert(TPB <= td_tpb_max<NMAX>(), "LDS budget");
+  __shared__ TdTileLds<NMAX> TW[TPB];
+  __shared__ __attribute__((aligned(16))) float Pon[N_PARAMS_PAD];
+  __shared__ __attribute__((aligned(16))) float Ptg[N_PARAMS_PAD];
+  const int wave = threadIdx.x >> 6;
+  const int tl = wave % TPB;
+  const bool online = wave < TPB;
+  TdTileLds<NMAX>& T = TW[tl];
+  WaveLds& L = online ? T.L : T.LT;
   const int N = A.N;
-  const Geom g = make_geom(blockIdx.x, N, A.S);
+  const Geom g = make_geom(blockIdx.x * TPB + tl, N, A.S);
   const int lane = g.lane, h = g.h;
-  float* slab = A.slabs + (size_t)blockIdx.x * (N_PARAMS + 1);
+  float* gslab = A.slabs + (size_t)blockIdx.x * (N_PARAMS + 1);
+  float* slab = &T.T[0][0];       // this tile's partial slab (after the products)
+  SWARM_STAMP(0);
 
+  // ---- weights: both images' loads issued first (one round trip)
+  ParamStage<128 * TPB> pon, ptg;
+  pon.load(A.params, threadIdx.x);
+  ptg.load(A.target, threadIdx.x);
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
   const uint32_t filled = A.ctrl->filled_slots;
   const uint32_t cap = (uint32_t)A.replay.capacity;
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
   const uint32_t n_graphs = valid_slots * (uint32_t)A.B;
   if (n_graphs < (uint32_t)A.S) {
-    for (int p = lane; p <= N_PARAMS; p += 64) slab[p] = 0.0f;
+    for (int p = threadIdx.x; p <= N_PARAMS; p += 128 * TPB) gslab[p] = 0.0f;
     return;
   }
-
+  SWARM_STAMP(1);
   // ---- sample (GraphReplayBuffer.sample: random.sample -> keyed permutation)
   uint32_t gid = 0;
-  if (g.valid) {
-    if (A.sample_in) gid = (uint32_t)A.sample_in[g.env];
-    else gid = sample_index((uint32_t)g.env, n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1,
-                            A.ctrl->tick);
-    if (A.sample_out && h == 0 && g.agent == 0) A.sample_out[g.env] = (int32_t)gid;
+  if (A.sample_in) {
+    gid = (uint32_t)A.sample_in[g.valid ? g.env : 0];
+  } else {
+    const SampleKey sk = sample_key(n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, A.ctrl->tick);
+    gid = sample_index((uint32_t)(g.valid ? g.env : 0), sk);
   }
+  if (A.sample_out && online && g.valid && h == 0 && g.agent == 0) A.sample_out[g.env] = (int32_t)gid;
+  SWARM_STAMP(2);
   const uint32_t slot = gid / (uint32_t)A.B, genv = gid % (uint32_t)A.B;
   const size_t ri = ((size_t)slot * A.B + genv) * N + g.agent;
-  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
-  float rew = 0.0f;
-  int act = 0;
-  if (g.valid) {
-    s0 = reinterpret_cast<const float4*>(A.replay.s)[ri];
-    s1 = reinterpret_cast<const float4*>(A.replay.s_next)[ri];
-    rew = A.replay.r[ri];
-    act = A.replay.a[ri];
-  }
+  const float4 st = reinterpret_cast<const float4*>(online ? A.replay.s : A.replay.s_next)[ri];
+  const float rew = A.replay.r[ri];
+  const int act = g.valid ? (int)A.replay.a[ri] : 0;
+  pon.store(Pon, threadIdx.x);
+  ptg.store(Ptg, threadIdx.x);
 
   FwdState F;
-  int mult[NMAX];
-  float c[NMAX];
-  auto features = [&](const float4& s) {
-    F.x[0] = s.x; F.x[1] = s.y; F.x[2] = s.z; F.x[3] = s.w;
-    F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)g.agent; F.x[7] = 0.0f;
-    if (!g.valid) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
-    }
-    if (h == 0) { L.px[g.v] = F.x[0]; L.py[g.v] = F.x[1]; }
-  };
-
-  // ---- target network on s' (train_gcn_dqn.py:120-121)
-  features(s1);
-  __syncthreads();
-  tile_forward<NMAX>(A.target, g, N, A.graph, A.k, A.conv, nullptr, L, F, mult, c);
-  float qmax = F.q[0];
-#pragma unroll
-  for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[a]);
-  const float y = rew + A.gamma * qmax;
-  __syncthreads();
-
-  // ---- online network on s (keeps activations)
-  features(s0);
-  __syncthreads();
-  tile_forward<NMAX>(A.params, g, N, A.graph, A.k, A.conv, nullptr, L, F, mult, c);
-  float qa = F.q[0];
-#pragma unroll
-  for (int a = 1; a < kActions; ++a) qa = (act == a) ? F.q[a] : qa;
-  const float delta = g.valid ? (qa - y) : 0.0f;
-  const float gq = delta * A.grad_scale;
+  F.x[0] = st.x; F.x[1] = st.y; F.x[2] = st.z; F.x[3] = st.w;
+  F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)g.agent; F.x[7] = 0.0f;
   if (!g.valid) {
 #pragma unroll
-    for (int u = 0; u < NMAX; ++u) c[u] = 0.0f;
+    for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
   }
-
-  const float* __restrict__ P = A.params;
-  // ---- MLP backward
-  float dZ[16], dT[16], dO[16];
-  {
-    float w2[16];
-    load_vec_acc(P + OFF_W2 + act * kHidden, h, w2);
+  if (h == 0) { L.px[g.v] = F.x[0]; L.py[g.v] = F.x[1]; }
+  int mult[NMAX];
+  float c[NMAX];
+  __syncthreads();
+  SWARM_STAMP(3);
+  // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121)
+  tile_forward<NMAX, 16>(online ? Pon : Ptg, g, N, A.graph, A.k, A.conv, nullptr, L, F, mult, c);
+  if (!online) {
+    float qmax = F.q[0];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float dR = w2[r] * gq;
-      dZ[r] = F.zr[r] > 0.0f ? dR : 0.0f;
+    for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[a]);
+    if (h == 0) T.y[g.v] = rew + A.gamma * qmax;
+  }
+  SWARM_STAMP(4);
+  __syncthreads();
+  SWARM_STAMP(5);
+
+  const float* P = Pon;
+  float delta = 0.0f;
+  float dO[16];
+  if (online) {
+    float qa = F.q[0];
+#pragma unroll
+    for (int a = 1; a < kActions; ++a) qa = (act == a) ? F.q[a] : qa;
+    delta = g.valid ? (qa - T.y[g.v]) : 0.0f;
+    const float gq = delta * A.grad_scale;
+    if (!g.valid) {
+#pragma unroll
+      for (int u = 0; u < NMAX; ++u) c[u] = 0.0f;
+    }
+    // ---- MLP backward
+    float dZ[16], dT[16];
+    {
+      float w2[16];
+      load_vec_acc(P + OFF_W2 + act * kHidden, h, w2);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float dR = w2[r] * gq;
+        dZ[r] = F.zr[r] > 0.0f ? dR : 0.0f;
+      }
+    }
+    mfma_lin32_t(P + OFF_W1, g, dZ, dT);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dO[r] = dT[r] * (1.0f - F.t[r] * F.t[r]);
+    SWARM_STAMP(6);
+    store_acc_row(T.T, g.v, h, F.t);
+    store_acc_row(T.R, g.v, h, F.zr);
+    store_acc_row(T.dZ, g.v, h, dZ);
+    store_acc_row(T.dO, g.v, h, dO);
+    if (h == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) T.X[g.v][k] = k < kFeat ? F.x[k] : 0.0f;
+      T.X[g.v][8] = 0.0f;
+      T.gq[g.v] = gq;
+      T.act[g.v] = act;
+      T.d2[g.v] = delta * delta;
+#pragma unroll
+      for (int u = 0; u < NMAX; ++u)
+        if (u < N) T.cm[g.v][u] = c[u];
     }
   }
-  mfma_lin32_t(P + OFF_W1, g, dZ, dT);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) dO[r] = dT[r] * (1.0f - F.t[r] * F.t[r]);
+  __syncthreads();   // images of every tile ready
+  SWARM_STAMP(7);
 
-  store_acc_row(T.T, g.v, h, F.t);
-  store_acc_row(T.R, g.v, h, F.zr);
-  store_acc_row(T.dZ, g.v, h, dZ);
-  store_acc_row(T.dO, g.v, h, dO);
-  if (h == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) T.X[g.v][k] = k < kFeat ? F.x[k] : 0.0f;
-    T.gq[g.v] = gq;
-    T.act[g.v] = act;
-    T.d2[g.v] = delta * delta;
-#pragma unroll
-    for (int u = 0; u < NMAX; ++u)
-      if (u < N) T.cm[g.v][u] = c[u];
-  } else {
-#pragma unroll
-    for (int k = 8; k < kTile; ++k) T.X[g.v][k] = 0.0f;
-  }
-  __syncthreads();
-
-  // ---- GAT backward (attention part)
+  const int col = lane & 31;
+  // target-wave products (registers) while the online wave does the GAT backward
+  f32x16 dW1 = {}, dW2 = {};
+  float s_bias = 0.0f, s_b1 = 0.0f, s_b2 = 0.0f, s_loss = 0.0f;
   float da_s = 0.0f, da_d = 0.0f;
-  if (A.conv == SWARM_CONV_GAT) {
+  if (!online) {
+    dW1 = mfma_nodesum(T.dZ, T.T, lane);                       // dW1[i][hid]
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {                             // dW2[a][hid]
+      const int n = 2 * s + h;
+      const float a = (T.act[n] == col) ? T.gq[n] : 0.0f;
+      dW2 = mfma32(a, T.R[n][col], dW2);
+    }
+    if (h == 0) {
+      for (int n = 0; n < kTile; ++n) s_bias = s_bias + T.dO[n][col];
+    } else {
+      for (int n = 0; n < kTile; ++n) s_b1 = s_b1 + T.dZ[n][col];
+    }
+    if (lane < kActions) {
+      for (int n = 0; n < kTile; ++n) s_b2 = s_b2 + (T.act[n] == lane ? T.gq[n] : 0.0f);
+    } else if (lane == 63) {
+      for (int n = 0; n < kTile; ++n) s_loss = s_loss + T.d2[n];
+    }
+  } else if (A.conv == SWARM_CONV_GAT) {
+    // ---- GAT backward (attention part), branch-free over the env's sources u
     float gu[NMAX];
-    float G = 0.0f;
 #pragma unroll
     for (int u = 0; u < NMAX; ++u) {
       gu[u] = 0.0f;
-      if (u < N && c[u] != 0.0f) {
+      if (u < N) {
         const float* row = &L.hs[g.base + u][4 * h];
         float p = 0.0f;
 #pragma unroll
@@ -196,15 +241,16 @@ __global__ __launch_bounds__(64) void td_kernel(TdArgs A) {
         gu[u] = p;
       }
     }
+    float G = 0.0f;
 #pragma unroll
     for (int u = 0; u < NMAX; ++u) {
       if (u < N) gu[u] = gu[u] + xor32(gu[u]);
-      if (u < N && c[u] != 0.0f) G = G + c[u] * gu[u];
+      if (u < N) G = G + c[u] * gu[u];
     }
 #pragma unroll
     for (int u = 0; u < NMAX; ++u) {
       float dpu = 0.0f;
-      if (u < N && c[u] != 0.0f) {
+      if (u < N) {
         const float de = c[u] * (gu[u] - G);
         const float pre = L.ssrc[g.base + u] + F.sdst;
         dpu = pre > 0.0f ? de : de * kLeakySlope;
@@ -212,21 +258,30 @@ __global__ __launch_bounds__(64) void td_kernel(TdArgs A) {
       da_d = da_d + dpu;
       if (u < N && h == 0) T.dp[g.v][u] = dpu;
     }
-    __syncthreads();
-    for (int w = 0; w < N; ++w) da_s = da_s + T.dp[g.base + w][g.agent];
-    if (!g.valid) { da_s = 0.0f; da_d = 0.0f; }
   }
-  // ---- dh = messages + attention-coefficient terms
-  float dh[16];
-  {
+  __syncthreads();   // dp ready
+  SWARM_STAMP(8);
+  if (online) {
+    if (A.conv == SWARM_CONV_GAT) {
+      float col_dp[NMAX];
+#pragma unroll
+      for (int w = 0; w < NMAX; ++w) col_dp[w] = T.dp[g.base + (w < N ? w : 0)][g.agent];
+#pragma unroll
+      for (int w = 0; w < NMAX; ++w)
+        if (w < N) da_s = da_s + col_dp[w];
+    }
+    if (!g.valid) { da_s = 0.0f; da_d = 0.0f; }
+    // ---- dh = messages + attention-coefficient terms
+    float dh[16];
     float as[16], ad[16];
     load_vec_acc(P + OFF_ATT_SRC, h, as);
     load_vec_acc(P + OFF_ATT_DST, h, ad);
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] = 0.0f;
-    for (int w = 0; w < N; ++w) {
-      const float cw = g.valid ? T.cm[g.base + w][g.agent] : 0.0f;   // c[target w][source me]
-      if (cw != 0.0f) {
+#pragma unroll
+    for (int w = 0; w < NMAX; ++w) {
+      if (w < N) {
+        const float cw = g.valid ? T.cm[g.base + w][g.agent] : 0.0f;   // c[target w][source me]
         const float* row = &T.dO[g.base + w][4 * h];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -240,173 +295,178 @@ __global__ __launch_bounds__(64) void td_kernel(TdArgs A) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) dh[r] = (dh[r] + da_s * as[r]) + da_d * ad[r];
+    store_acc_row(T.dH, g.v, h, dh);
+    if (h == 0) { T.das[g.v] = da_s; T.dad[g.v] = da_d; }
   }
-  store_acc_row(T.dH, g.v, h, dh);
-  if (h == 0) { T.das[g.v] = da_s; T.dad[g.v] = da_d; }
-  __syncthreads();
-
-  // ---- parameter gradients summed over the tile's node slots
-  const int col = lane & 31;
-  {
-    const f32x16 d = mfma_nodesum(T.dZ, T.T, lane);            // dW1[i][hid]
+  __syncthreads();   // dH ready
+  SWARM_STAMP(9);
+  f32x16 dW = {};
+  float s_as = 0.0f, s_ad = 0.0f;
+  if (online) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) slab[OFF_W1 + acc_row(r, h) * kHidden + col] = d[r];
-  }
-  {
-    f32x16 acc = {};                                             // dW2[a][hid]
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < 16; ++s) {                             // dW[hid][k]
       const int n = 2 * s + h;
-      const float a = (T.act[n] == col) ? T.gq[n] : 0.0f;
-      acc = mfma32(a, T.R[n][col], acc);
+      dW = mfma32(T.dH[n][col], col < 8 ? T.X[n][col] : 0.0f, dW);
     }
+    if (h == 0) {
+      for (int n = 0; n < kTile; ++n) s_as = s_as + T.das[n] * L.hs[n][col];
+    } else {
+      for (int n = 0; n < kTile; ++n) s_ad = s_ad + T.dad[n] * L.hs[n][col];
+    }
+  }
+  SWARM_STAMP(10);
+  __syncthreads();   // every image read done: the image area becomes the partial slab
+  if (online) {
+    if (col < kFeat) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) slab[OFF_W + acc_row(r, h) * kFeat + col] = dW[r];
+    }
+    if (h == 0) slab[OFF_ATT_SRC + col] = s_as;
+    else        slab[OFF_ATT_DST + col] = s_ad;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) slab[OFF_W1 + acc_row(r, h) * kHidden + col] = dW1[r];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int a = acc_row(r, h);
-      if (a < kActions) slab[OFF_W2 + a * kHidden + col] = acc[r];
+      if (a < kActions) slab[OFF_W2 + a * kHidden + col] = dW2[r];
     }
+    if (h == 0) slab[OFF_BIAS + col] = s_bias;
+    else        slab[OFF_B1 + col] = s_b1;
+    if (lane < kActions) slab[OFF_B2 + lane] = s_b2;
+    else if (lane == 63) slab[N_PARAMS] = s_loss;
   }
-  {
-    const f32x16 d = mfma_nodesum(T.dH, T.X, lane);            // dW[hid][k]
-    if (col < kFeat) {
+  __syncthreads();
+  SWARM_STAMP(11);
+  // fixed-order sum of the block's TPB partial slabs -> one global slab
+  for (int p = threadIdx.x; p <= N_PARAMS; p += 128 * TPB) {
+    float acc = (&TW[0].T[0][0])[p];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) slab[OFF_W + acc_row(r, h) * kFeat + col] = d[r];
-    }
+    for (int w = 1; w < TPB; ++w) acc = acc + (&TW[w].T[0][0])[p];
+    gslab[p] = acc;
   }
-  {
-    float s1v = 0.0f, s2v = 0.0f;
-    if (h == 0) {
-      for (int n = 0; n < kTile; ++n) { s1v = s1v + T.dO[n][col]; s2v = s2v + T.das[n] * L.hs[n][col]; }
-      slab[OFF_BIAS + col] = s1v;
-      slab[OFF_ATT_SRC + col] = s2v;
-    } else {
-      for (int n = 0; n < kTile; ++n) { s1v = s1v + T.dZ[n][col]; s2v = s2v + T.dad[n] * L.hs[n][col]; }
-      slab[OFF_B1 + col] = s1v;
-      slab[OFF_ATT_DST + col] = s2v;
-    }
-  }
-  if (lane < kActions) {
-    float s = 0.0f;
-    for (int n = 0; n < kTile; ++n) s = s + (T.act[n] == lane ? T.gq[n] : 0.0f);
-    slab[OFF_B2 + lane] = s;
-  } else if (lane == 63) {
-    float s = 0.0f;
-    for (int n = 0; n < kTile; ++n) s = s + T.d2[n];
-    slab[N_PARAMS] = s;
-  }
+  SWARM_STAMP(12);
 }
 
 // ---------------------------------------------------------------- slab reduction
 // block = 256 threads covers 64 columns; thread (col, part) sums a contiguous quarter
 // of the slabs, quarters combined in order: fixed order -> bitwise reproducible.
-__global__ __launch_bounds__(256) void grad_reduce_kernel(int n_slabs, const float* __restrict__ slabs,
-                                                          float* __restrict__ grad) {
+struct ReduceArgs {
+  int n_slabs;
+  const float* slabs;
+  float* grad;
+  int advance;            // fused tick: copy *_nxt -> *_cur and advance ctrl
+  swarm_learner lr;
+  swarm_ctrl* ctrl;
+  int capacity, B, N, batch;
+  float beta1, beta2;
+};
+
+__global__ __launch_bounds__(256) void grad_reduce_kernel(ReduceArgs A) {
   __shared__ float part[4][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int q = threadIdx.x >> 6;
-  const int per = (n_slabs + 3) / 4;
-  const int b0 = q * per, b1 = min(n_slabs, b0 + per);
+  const int per = (A.n_slabs + 3) / 4;
+  const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
   float s = 0.0f;
-  if (col <= N_PARAMS)
-    for (int b = b0; b < b1; ++b) s = s + slabs[(size_t)b * (N_PARAMS + 1) + col];
+  if (col <= N_PARAMS) {
+    for (int b = b0; b < b1; b += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = (b + j < b1) ? A.slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s = s + v[j];
+    }
+  }
+  if (A.advance && col < N_PARAMS) {   // ping-pong copy-back, one array per quarter
+    if (q == 0) A.lr.w_cur[col] = A.lr.w_nxt[col];
+    else if (q == 1) A.lr.m_cur[col] = A.lr.m_nxt[col];
+    else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
+  }
   part[q][threadIdx.x & 63] = s;
   __syncthreads();
   if (q == 0 && col <= N_PARAMS) {
     const int c = threadIdx.x & 63;
-    grad[col] = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
+    const float tot = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
+    A.grad[col] = tot;
+    if (A.advance && col == N_PARAMS) {   // one thread: record the pending update, advance the tick
+      swarm_ctrl* C = A.ctrl;
+      const uint32_t cap = (uint32_t)A.capacity;
+      const uint32_t filled = C->filled_slots;
+      const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
+      const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
+      if (C->trained) {                                   // applied by this tick's act kernel
+        C->adam_step = C->adam_step + 1;
+        ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * (double)A.beta1);
+        ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * (double)A.beta2);
+      }
+      C->trained = trained;
+      C->loss = trained ? tot / (float)((size_t)A.batch * A.N) : 0.0f;
+      C->tick = C->tick + 1;
+      C->write_slot = (C->write_slot + 1) % cap;
+      C->filled_slots = valid_slots;
+    }
   }
 }
 
 // ---------------------------------------------------------------- clip + Adam + target sync
+// Unfused path (swarm_adam_step): apply now, then advance ctrl.  Flush path
+// (swarm_adam_flush): apply a pending fused update in place, no advance.
 struct AdamArgs {
-  float lr, beta1, beta2, eps, max_norm;
-  int batch, update_every, world, B, N;
+  swarm_adam_cfg hp;
+  int B, N, capacity, flush;
   float* params;
   float* target;
   float* m;
   float* v;
   const float* grad;
   swarm_ctrl* ctrl;
-  int capacity;
 };
 
-__device__ inline float block_sum_1024(float x, float* sh) {
-  const int t = threadIdx.x;
-  for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);
-  __syncthreads();
-  if ((t & 63) == 0) sh[t >> 6] = x;
-  __syncthreads();
-  float s = 0.0f;
-  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s = s + sh[w];
-  return s;
-}
-
-__global__ __launch_bounds__(1024) void adam_kernel(AdamArgs A) {
-  __shared__ float sh[16];
-  __shared__ float tnorm[8];
-  const int t = threadIdx.x;
+__global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
+  __shared__ float red[8 * (kAdamNT / 64) + 8];
+  const int tid = threadIdx.x;
+  AdamRegs R;
+  R.load(A.grad, A.params, A.m, A.v, tid);
+  const float loss_sum = A.grad[N_PARAMS];
   swarm_ctrl* C = A.ctrl;
-  const uint32_t filled = C->filled_slots;
   const uint32_t cap = (uint32_t)A.capacity;
+  const uint32_t filled = C->filled_slots;
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
-  const bool train = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch;
   const uint32_t tick = C->tick;
-  const uint32_t step = C->adam_step;
-  __syncthreads();
+  const uint32_t step = C->adam_step + 1;
+  const double b1pow = ctrl_get_double(C, CTRL_B1POW) * (double)A.hp.beta1;
+  const double b2pow = ctrl_get_double(C, CTRL_B2POW) * (double)A.hp.beta2;
+  const bool train = A.flush ? (C->trained != 0u) : (valid_slots * (uint32_t)A.B >= (uint32_t)A.hp.batch);
+  // target sync: unfused = after the TD step of tick `tick` ((tick+1) % every); flush = the
+  // fused tick already advanced ctrl, so the pending update belongs to tick - 1
+  const bool sync = ((A.flush ? tick : tick + 1) % (uint32_t)A.hp.update_target_every) == 0u;
+  __syncthreads();   // every thread has read ctrl before thread 0 rewrites it
+  float gn = 0.0f;
   if (train) {
-    const float inv_w = 1.0f / (float)A.world;
-    // per-tensor L2 norms, then the norm of norms (torch clip_grad_norm_)
-    const int offs[9] = {OFF_ATT_SRC, OFF_ATT_DST, OFF_BIAS, OFF_W, OFF_W1, OFF_B1, OFF_W2, OFF_B2, N_PARAMS};
-    for (int ti = 0; ti < 8; ++ti) {
-      float ss = 0.0f;
-      for (int p = offs[ti] + t; p < offs[ti + 1]; p += blockDim.x) {
-        const float gg = A.world > 1 ? A.grad[p] * inv_w : A.grad[p];
-        ss = ss + gg * gg;
-      }
-      const float tot = block_sum_1024(ss, sh);
-      if (t == 0) tnorm[ti] = sqrtf(tot);
-      __syncthreads();
-    }
-    float nn = 0.0f;
-    for (int ti = 0; ti < 8; ++ti) nn = nn + tnorm[ti] * tnorm[ti];
-    const float total_norm = sqrtf(nn);
-    const float coef = A.max_norm / (total_norm + 1e-6f);
-    const float clamped = coef < 1.0f ? coef : 1.0f;
-    const double stepd = (double)(step + 1);
-    const double bc1 = 1.0 - pow((double)A.beta1, stepd);
-    const double bc2 = 1.0 - pow((double)A.beta2, stepd);
-    const float step_size = (float)((double)A.lr / bc1);
-    const float bc2_sqrt = (float)sqrt(bc2);
-    const float one_m_b1 = (float)(1.0 - (double)A.beta1);
-    const float one_m_b2 = (float)(1.0 - (double)A.beta2);
-    const bool sync = ((tick + 1) % (uint32_t)A.update_every) == 0u;
-    for (int p = t; p < N_PARAMS; p += blockDim.x) {
-      float gg = A.world > 1 ? A.grad[p] * inv_w : A.grad[p];
-      gg = gg * clamped;
-      float m = A.m[p], v = A.v[p];
-      m = m + one_m_b1 * (gg - m);                       // exp_avg.lerp_(grad, 1-beta1)
-      v = v * A.beta2;
-      v = v + one_m_b2 * gg * gg;                        // addcmul_(grad, grad, 1-beta2)
-      const float denom = sqrtf(v) / bc2_sqrt + A.eps;
-      const float np = A.params[p] + (-step_size) * (m / denom);
-      A.m[p] = m; A.v[p] = v; A.params[p] = np;
-      if (sync) A.target[p] = np;
-    }
-    if (t == 0) {
-      C->adam_step = step + 1;
-      C->loss = A.grad[N_PARAMS] / (float)((size_t)A.batch * A.N) / (float)A.world;
-      C->grad_norm = total_norm;
-      C->trained = 1u;
-    }
-  } else if (t == 0) {
-    C->loss = 0.0f;
-    C->grad_norm = 0.0f;
-    C->trained = 0u;
+    gn = adam_apply(R, A.hp, b1pow, b2pow, tid, red);
+    store4(A.params, R.w, R.wt, tid);
+    store4(A.m, R.m, R.mt, tid);
+    store4(A.v, R.v, R.vt, tid);
+    if (sync) store4(A.target, R.w, R.wt, tid);
   }
-  if (t == 0) {
-    C->tick = tick + 1;
-    C->write_slot = (C->write_slot + 1) % cap;
-    C->filled_slots = filled + 1 < cap ? filled + 1 : cap;
+  if (tid == 0) {
+    if (train) {
+      C->adam_step = step;
+      C->grad_norm = gn;
+      ctrl_set_double(C, CTRL_B1POW, b1pow);
+      ctrl_set_double(C, CTRL_B2POW, b2pow);
+    }
+    if (A.flush) {
+      C->trained = 0u;
+    } else {
+      C->trained = 0u;   // applied now: nothing pending
+      C->loss = train ? loss_sum / (float)((size_t)A.hp.batch * A.N) / (float)A.hp.world_size : 0.0f;
+      if (!train) C->grad_norm = 0.0f;
+      C->tick = tick + 1;
+      C->write_slot = (C->write_slot + 1) % cap;
+      C->filled_slots = valid_slots;
+    }
   }
 }
 
@@ -422,10 +482,24 @@ __global__ void ctrl_advance_kernel(swarm_ctrl* C, int capacity) {
 using namespace swarm;
 
 namespace {
-int td_blocks(const swarm_config* cfg, int batch) {
+int td_tiles(const swarm_config* cfg, int batch) {
   const int E = kTile / cfg->n_agents;
   return (batch + E - 1) / E;
 }
+// tiles per TD block (each tile = online wave + target wave); SWARM_TD_TPB=1|2|3 overrides
+int td_tpb_rt(int N) {
+  static int env = [] { const char* e = getenv("SWARM_TD_TPB"); return e ? atoi(e) : 0; }();
+  const int mx = N <= 16 ? 3 : 2;
+  int t = (env >= 1 && env <= 3) ? env : 2;
+  return t < mx ? t : mx;
+}
+int td_blocks(const swarm_config* cfg, int batch) {
+  const int w = td_tpb_rt(cfg->n_agents);
+  return (td_tiles(cfg, batch) + w - 1) / w;
+}
+int td_max_blocks(const swarm_config* cfg, int batch) { return td_tiles(cfg, batch); }
+}  // namespace
+namespace {
 int check_td(const swarm_config* c, const swarm_adam_cfg* hp) {
   if (!c || !hp || c->n_agents < 1 || c->n_agents > 32 || c->n_envs < 1 || hp->batch < 1) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_DENSE) return SWARM_E_BADARG;
@@ -439,7 +513,7 @@ extern "C" {
 
 int64_t swarm_td_workspace_floats(const swarm_config* cfg, int32_t batch) {
   if (!cfg || cfg->n_agents < 1 || cfg->n_agents > 32 || batch < 1) return SWARM_E_BADARG;
-  return (int64_t)td_blocks(cfg, batch) * (N_PARAMS + 1);
+  return (int64_t)td_max_blocks(cfg, batch) * (N_PARAMS + 1);
 }
 
 int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* params, const float* target,
@@ -457,18 +531,47 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.grad_scale = (float)(2.0 / ((double)hp->batch * (double)cfg->n_agents));
   const int nb = td_blocks(cfg, hp->batch);
   hipStream_t st = (hipStream_t)stream;
-  if (a.N <= 8) hipLaunchKernelGGL((td_kernel<8>), dim3(nb), dim3(64), 0, st, a);
-  else if (a.N <= 16) hipLaunchKernelGGL((td_kernel<16>), dim3(nb), dim3(64), 0, st, a);
-  else hipLaunchKernelGGL((td_kernel<32>), dim3(nb), dim3(64), 0, st, a);
+  const int w = td_tpb_rt(a.N);
+#define SW_TD(NM, W) hipLaunchKernelGGL((td_kernel<NM, W>), dim3(nb), dim3(128 * W), 0, st, a)
+  if (a.N <= 8) { if (w == 1) SW_TD(8, 1); else if (w == 2) SW_TD(8, 2); else SW_TD(8, 3); }
+  else if (a.N <= 16) { if (w == 1) SW_TD(16, 1); else if (w == 2) SW_TD(16, 2); else SW_TD(16, 3); }
+  else { if (w == 1) SW_TD(32, 1); else SW_TD(32, 2); }
+#undef SW_TD
   return (int)hipGetLastError();
 }
+
+#if SWARM_STAMPS
+int swarm_dbg_stamps_td(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_swarm_stamps), &p, sizeof(p)); }
+#endif
 
 int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, float* grad,
                       void* stream) {
   if (int e = check_td(cfg, hp)) return e;
-  const int nb = td_blocks(cfg, hp->batch);
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(256), 0, (hipStream_t)stream, nb,
-                     slabs, grad);
+  ReduceArgs a = {};
+  a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = grad;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
+                         int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
+  if (int e = check_td(cfg, hp)) return e;
+  if (!lr || !ctrl || replay_capacity < 1) return SWARM_E_BADARG;
+  ReduceArgs a = {};
+  a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = lr->grad;
+  a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
+  a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
+  a.beta1 = hp->beta1; a.beta2 = hp->beta2;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+static int launch_adam(const swarm_config* cfg, const swarm_adam_cfg* hp, float* params, float* target, float* m,
+                       float* v, const float* grad, int32_t cap, swarm_ctrl* ctrl, int flush, void* stream) {
+  AdamArgs a = {};
+  a.hp = *hp; a.B = cfg->n_envs; a.N = cfg->n_agents; a.capacity = cap; a.flush = flush;
+  a.params = params; a.target = target; a.m = m; a.v = v; a.grad = grad; a.ctrl = ctrl;
+  hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(kAdamNT), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
@@ -476,14 +579,14 @@ int swarm_adam_step(const swarm_config* cfg, const swarm_adam_cfg* hp, float* pa
                     float* adam_v, const float* grad, int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
   if (int e = check_td(cfg, hp)) return e;
   if (!params || !target || !adam_m || !adam_v || !grad || !ctrl || replay_capacity < 1) return SWARM_E_BADARG;
-  AdamArgs a = {};
-  a.lr = hp->lr; a.beta1 = hp->beta1; a.beta2 = hp->beta2; a.eps = hp->eps; a.max_norm = hp->max_norm;
-  a.batch = hp->batch; a.update_every = hp->update_target_every; a.world = hp->world_size;
-  a.B = cfg->n_envs; a.N = cfg->n_agents;
-  a.params = params; a.target = target; a.m = adam_m; a.v = adam_v; a.grad = grad; a.ctrl = ctrl;
-  a.capacity = replay_capacity;
-  hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
-  return (int)hipGetLastError();
+  return launch_adam(cfg, hp, params, target, adam_m, adam_v, grad, replay_capacity, ctrl, 0, stream);
+}
+
+int swarm_adam_flush(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, swarm_ctrl* ctrl,
+                     void* stream) {
+  if (int e = check_td(cfg, hp)) return e;
+  if (!lr || !ctrl) return SWARM_E_BADARG;
+  return launch_adam(cfg, hp, lr->w_cur, lr->target, lr->m_cur, lr->v_cur, lr->grad, 1, ctrl, 1, stream);
 }
 
 int swarm_ctrl_advance(const swarm_config* cfg, const swarm_replay* replay, swarm_ctrl* ctrl, void* stream) {

@@ -52,6 +52,35 @@ __device__ inline Geom make_geom(int tile, int N, int B) {
 }
 
 // ---------------------------------------------------------------- weights
+// Copy the flat parameter vector into an LDS image once per block (every weight
+// read of the forward/backward then hits LDS instead of a global round trip).
+// All global loads are issued before the first LDS write and none sits behind a
+// branch (clamped index), so the copy costs ONE memory round trip, not NJ.
+template <int NT>
+struct ParamStage {
+  static constexpr int NF4 = N_PARAMS / 4;            // 418 full float4 (floats 0..1671)
+  static constexpr int NJ = (NF4 + NT - 1) / NT;
+  float4 v[NJ];
+  float tail;
+  __device__ inline void load(const float* __restrict__ g, int tid) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = min(tid + j * NT, NF4 - 1);
+      v[j] = reinterpret_cast<const float4*>(g)[i];
+    }
+    tail = g[N_PARAMS - 1];
+  }
+  __device__ inline void store(float* __restrict__ lds, int tid) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = tid + j * NT;
+      if (i < NF4) reinterpret_cast<float4*>(lds)[i] = v[j];
+    }
+    if (tid == 0) *reinterpret_cast<float4*>(lds + 4 * NF4) = make_float4(tail, 0.0f, 0.0f, 0.0f);
+  }
+};
+static_assert(ParamStage<64>::NF4 * 4 + 1 == N_PARAMS && N_PARAMS_PAD == ParamStage<64>::NF4 * 4 + 4, "tail");
+
 // float4 view of a 32-vector at the acc layout positions acc_row(4q..4q+3, h) = 8q+4h..+3
 __device__ inline void load_vec_acc(const float* __restrict__ p, int h, float out[16]) {
 #pragma unroll
@@ -152,29 +181,26 @@ __device__ inline void conv_aggregate(const float* __restrict__ P, const Geom& g
                                       WaveLds& L, const int mult[NMAX], float sdst, float c[NMAX],
                                       float out[16]) {
   if (conv == SWARM_CONV_GAT) {
+    // branch-free over the env's sources u: every LDS read issued together, non-edges masked
     float e[NMAX];
     float emax = -INFINITY;
 #pragma unroll
     for (int u = 0; u < NMAX; ++u) {
-      e[u] = 0.0f;
-      if (u < N && mult[u] > 0) {
-        e[u] = leaky(L.ssrc[g.base + u] + sdst);
-        emax = fmaxf(emax, e[u]);
-      }
+      const bool on = (u < N) && mult[u] > 0;
+      e[u] = leaky(L.ssrc[g.base + (u < N ? u : 0)] + sdst);
+      emax = on ? fmaxf(emax, e[u]) : emax;
     }
     float den = 0.0f;
 #pragma unroll
     for (int u = 0; u < NMAX; ++u) {
-      c[u] = 0.0f;
-      if (u < N && mult[u] > 0) {
-        e[u] = expf(e[u] - emax);
-        den = den + (float)mult[u] * e[u];
-      }
+      const bool on = (u < N) && mult[u] > 0;
+      e[u] = on ? __expf(e[u] - emax) : 0.0f;
+      den = den + (float)mult[u] * e[u];
     }
     den = den + 1e-16f;
+    const float inv = 1.0f / den;
 #pragma unroll
-    for (int u = 0; u < NMAX; ++u)
-      if (u < N && mult[u] > 0) c[u] = (float)mult[u] * (e[u] / den);
+    for (int u = 0; u < NMAX; ++u) c[u] = (float)mult[u] * (e[u] * inv);
   } else {
     // GCNConv (a13, parity unpinned): self loops collapse to weight 1, deg on targets
     float deg = 0.0f;
@@ -201,7 +227,7 @@ __device__ inline void conv_aggregate(const float* __restrict__ P, const Geom& g
   for (int r = 0; r < 16; ++r) out[r] = 0.0f;
 #pragma unroll
   for (int u = 0; u < NMAX; ++u) {
-    if (u < N && c[u] != 0.0f) {
+    if (u < N) {   // uniform condition; c[u] == 0 for non-edges
       const float* row = &L.hs[g.base + u][4 * g.h];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -217,17 +243,29 @@ __device__ inline void conv_aggregate(const float* __restrict__ P, const Geom& g
   for (int r = 0; r < 16; ++r) out[r] = out[r] + bias[r];
 }
 
-// lin2 on the VALU: half-wave partial dot + xor-32 exchange
-__device__ inline void lin2_valu(const float* __restrict__ P, const Geom& g, const float zr[16], float q[kActions]) {
+// lin2 on MFMA: Q^T = W2 R^T with W2 zero-padded to 32 rows (A row a = l&31 < 9);
+// result rows a = acc_row(r, h): half 0 holds a = 0..3 and 8, half 1 holds a = 4..7,
+// exchanged with one xor-32 swap per value.
+__device__ inline void lin2_mfma(const float* __restrict__ P, const Geom& g, const float zr[16], float q[kActions]) {
+  float a[16];
+  const int row = g.v < kActions ? g.v : 0;
+  load_vec_acc(P + OFF_W2 + row * kHidden, g.h, a);
+  if (g.v >= kActions) {
 #pragma unroll
-  for (int a = 0; a < kActions; ++a) {
-    float w[16];
-    load_vec_acc(P + OFF_W2 + a * kHidden, g.h, w);
-    float p = 0.0f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) p = p + zr[r] * w[r];
-    q[a] = (p + xor32(p)) + P[OFF_B2 + a];
+    for (int s = 0; s < 16; ++s) a[s] = 0.0f;
   }
+  f32x16 acc = {};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(a[s], zr[s], acc);
+  // own: h0 -> {0,1,2,3,8} at r {0,1,2,3,4}; h1 -> {4,5,6,7} at r {0,1,2,3}
+  const float o0 = acc[0], o1 = acc[1], o2 = acc[2], o3 = acc[3], o4 = acc[4];
+  const float p0 = xor32(o0), p1 = xor32(o1), p2 = xor32(o2), p3 = xor32(o3), p4 = xor32(o4);
+  float v[kActions];
+  v[0] = g.h ? p0 : o0; v[1] = g.h ? p1 : o1; v[2] = g.h ? p2 : o2; v[3] = g.h ? p3 : o3;
+  v[4] = g.h ? o0 : p0; v[5] = g.h ? o1 : p1; v[6] = g.h ? o2 : p2; v[7] = g.h ? o3 : p3;
+  v[8] = g.h ? p4 : o4;
+#pragma unroll
+  for (int i = 0; i < kActions; ++i) q[i] = v[i] + P[OFF_B2 + i];
 }
 
 __device__ inline int argmax9(const float q[kActions]) {
@@ -241,10 +279,11 @@ __device__ inline int argmax9(const float q[kActions]) {
 
 // Full GCN.forward for the tile.  Requires L.px/py written (kNN) for graph == KNN.
 // Contains __syncthreads(): every lane of the block must call it.
-template <int NMAX>
+template <int NMAX, int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
 __device__ inline void tile_forward(const float* __restrict__ P, const Geom& g, int N, int graph, int k,
                                     int conv, const uint8_t* __restrict__ dense, WaveLds& L,
                                     FwdState& F, int mult[NMAX], float c[NMAX]) {
+#define TF_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
   mfma_lin0(P, g, F.x, F.hreg);
   float as[16], ad[16];
   load_vec_acc(P + OFF_ATT_SRC, g.h, as);
@@ -263,12 +302,16 @@ __device__ inline void tile_forward(const float* __restrict__ P, const Geom& g, 
     const uint32_t m = g.valid ? knn_row<NMAX>(g, N, k, L) : 0u;
     if (g.h == 0) L.knn[g.v] = m;
   }
+  TF_STAMP(0);
   __syncthreads();
   graph_mult<NMAX>(g, N, graph, L, dense, mult);
+  TF_STAMP(1);
   float out[16];
   conv_aggregate<NMAX>(P, g, N, conv, L, mult, F.sdst, c, out);
+  TF_STAMP(2);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) F.t[r] = tanhf(out[r]);
+  for (int r = 0; r < 16; ++r) F.t[r] = tanh_fast(out[r]);
+  TF_STAMP(3);
   float z[16], b1[16];
   mfma_lin32(P + OFF_W1, g, F.t, z);
   load_vec_acc(P + OFF_B1, g.h, b1);
@@ -277,7 +320,10 @@ __device__ inline void tile_forward(const float* __restrict__ P, const Geom& g, 
     const float zz = z[r] + b1[r];
     F.zr[r] = zz > 0.0f ? zz : 0.0f;
   }
-  lin2_valu(P, g, F.zr, F.q);
+  TF_STAMP(4);
+  lin2_mfma(P, g, F.zr, F.q);
+  TF_STAMP(5);
+#undef TF_STAMP
 }
 
 // ---------------------------------------------------------------- env step (one agent)
@@ -293,6 +339,9 @@ struct StepOut {
 template <int NMAX, typename PosFn>
 __device__ inline StepOut agent_step(int scenario, int N, int agent, float px, float py, float vx, float vy,
                                      int action, PosFn pos) {
+  float ux[NMAX], uy[NMAX];
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u) pos(u < N ? u : 0, ux[u], uy[u]);   // all reads issued first
   float fx = 0.0f + action_level(action / 3);
   float fy = 0.0f + action_level(action % 3);
   if (scenario == SWARM_OBSTACLE_AVOIDANCE) {
@@ -302,11 +351,9 @@ __device__ inline StepOut agent_step(int scenario, int N, int agent, float px, f
   }
 #pragma unroll
   for (int u = 0; u < NMAX; ++u) {
-    if (u < N && u != agent) {
-      float ux, uy;
-      pos(u, ux, uy);
+    if (u < N) {
       float gx, gy;
-      pair_force(px - ux, py - uy, gx, gy);
+      pair_force(px - ux[u], py - uy[u], gx, gy);   // u == agent: dist 0 < 1e-6 -> exactly 0
       fx = fx + gx; fy = fy + gy;
     }
   }

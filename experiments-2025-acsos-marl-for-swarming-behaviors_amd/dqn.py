@@ -128,6 +128,7 @@ class DQNTrainer:
         return create_graph_from_observations(observations)
 
     def _sync_models(self):
+        self.engine.flush()
         self.model.load_state_dict(unflatten_params(self.engine.params.detach().cpu()))
         self.target_model.load_state_dict(unflatten_params(self.engine.target.detach().cpu()))
 

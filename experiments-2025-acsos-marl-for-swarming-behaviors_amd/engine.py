@@ -1,13 +1,19 @@
 """SwarmEngine: one rank's shard of vectorised swarm environments plus the DQN learner,
 all resident in HBM, driven through libswarm_hip.so.
 
-One training tick (the reference's hot loop, src/training/train_gcn_dqn.py:153-178):
+One fused training tick (the reference's hot loop, src/training/train_gcn_dqn.py:153-178):
 
-    swarm_act_step    graph -> GAT Q -> eps-greedy -> env.step -> replay push      (1 launch)
-    swarm_td_grad     sample -> target fwd -> online fwd -> TD loss -> backward      (1 launch)
-    swarm_grad_reduce deterministic slab sum                                         (1 launch)
+    swarm_train_act_step  [clip + Adam of the previous tick's gradient, target sync]
+                          graph -> GAT Q -> eps-greedy -> env.step -> replay push     (1 launch)
+    swarm_td_grad         sample -> target fwd -> online fwd -> TD loss -> backward    (1 launch)
+    swarm_reduce_advance  deterministic slab sum, ping-pong copy-back, ctrl advance    (1 launch)
     [all_reduce(grad) over RCCL when world_size > 1]
-    swarm_adam_step   clip_grad_norm_ + Adam + target sync + ctrl advance            (1 launch)
+
+The optimizer step of tick t runs at the start of tick t+1's acting launch (before any
+use of the weights), so every weight the reference would use is used; ``flush()``
+applies the last pending step.  The unfused sequence (``act`` + ``td_update``:
+act / td_grad / grad_reduce / adam_step) is kept for API calls and as the parity
+reference of the fused one (bit-identical, tests/test_gpu_parity.py).
 
 Every launch goes to torch's current stream, so a run of ticks can be captured
 once into a hipGraph (``capture``) and replayed.  There is no CPU fallback.
@@ -20,7 +26,8 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import CTRL, N_PARAMS, SwarmActOut, SwarmAdamCfg, SwarmConfig, SwarmReplay, check, ptr, stream_ptr
+from ._lib import (CTRL, N_PARAMS, SwarmActOut, SwarmAdamCfg, SwarmConfig, SwarmLearner, SwarmReplay, check, ptr,
+                   stream_ptr)
 
 SCENARIOS = {"GoTo": _lib.SWARM_GOTO, "ObstacleAvoidance": _lib.SWARM_OBSTACLE_AVOIDANCE,
              "go_to": _lib.SWARM_GOTO, "obstacle_avoidance": _lib.SWARM_OBSTACLE_AVOIDANCE}
@@ -103,12 +110,18 @@ class SwarmEngine:
             params = glorot_init(g)
         elif isinstance(params, dict):
             params = flatten_state_dict(params)
-        self.params = params.detach().to(**f32).clone().contiguous()
-        assert self.params.numel() == N_PARAMS
-        self.target = self.params.clone()
-        self.adam_m = torch.zeros(N_PARAMS, **f32)
-        self.adam_v = torch.zeros(N_PARAMS, **f32)
+        p0 = params.detach().to(**f32).reshape(-1)
+        assert p0.numel() == N_PARAMS
+        # learner buffers: [w_cur, w_nxt, m_cur, m_nxt, v_cur, v_nxt, target] rows + grad
+        self._lrn = torch.zeros(7, N_PARAMS + 3, **f32)       # +3: rows stay 16-B aligned
+        self.params, self.w_nxt = self._lrn[0, :N_PARAMS], self._lrn[1, :N_PARAMS]
+        self.adam_m, self.m_nxt = self._lrn[2, :N_PARAMS], self._lrn[3, :N_PARAMS]
+        self.adam_v, self.v_nxt = self._lrn[4, :N_PARAMS], self._lrn[5, :N_PARAMS]
+        self.target = self._lrn[6, :N_PARAMS]
+        self.params.copy_(p0)
+        self.target.copy_(p0)
         self.ctrl = torch.zeros(_lib.CTRL_WORDS, dtype=torch.int32, device=dev)
+        self.ctrl.view(torch.float64)[5:7] = 1.0     # words 10-13: beta1^0, beta2^0
         self.set_eps(eps)
         self.episode = 0
         cap = max(1, -(-replay_capacity // n_envs)) if learn else 1
@@ -122,7 +135,8 @@ class SwarmEngine:
         if ws < 0:
             check(int(ws), "swarm_td_workspace_floats")
         self.slabs = torch.zeros(int(ws), **f32)
-        self.grad = torch.zeros(N_PARAMS + 1, **f32)
+        self.grad = torch.zeros(N_PARAMS + 3, **f32)
+        self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         # per-tick outputs
         self.q = torch.zeros(n_envs, n_agents, 9, **f32)
         self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
@@ -206,14 +220,34 @@ class SwarmEngine:
                                        ptr(self.adam_m), ptr(self.adam_v), ptr(self.grad), self.capacity,
                                        ptr(self.ctrl), stream_ptr()), "swarm_adam_step")
 
+    def flush(self):
+        """Apply a pending fused optimizer step to the current weights (no-op if none)."""
+        check(self.lib.swarm_adam_flush(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
+                                        ptr(self.ctrl), stream_ptr()), "swarm_adam_flush")
+
     def td_update(self, sample_in=None, sample_out=None):
+        """Unfused TD update (API path): applies the optimizer step immediately."""
+        self.flush()
         self.td_grad(sample_in, sample_out)
         self.allreduce_grad()
         self.adam()
 
-    def train_tick(self, full_out: bool = False):
+    def train_tick_unfused(self, full_out: bool = False):
         self.act(push=True, full_out=full_out)
         self.td_update()
+
+    def train_tick(self, full_out: bool = False):
+        """Fused training tick: 3 launches (+ an RCCL all-reduce when world_size > 1)."""
+        cfg, hp = ctypes_ref(self.cfg), ctypes_ref(self.hp)
+        check(self.lib.swarm_train_act_step(cfg, hp, ctypes_ref(self.learner), ptr(self.state),
+                                            ctypes_ref(self.replay), ptr(self.ctrl),
+                                            ctypes_ref(self.out if full_out else self.out_min), stream_ptr()),
+              "swarm_train_act_step")
+        check(self.lib.swarm_td_grad(cfg, hp, ptr(self.w_nxt), ptr(self.target), ctypes_ref(self.replay),
+                                     ptr(self.ctrl), None, None, ptr(self.slabs), stream_ptr()), "swarm_td_grad")
+        check(self.lib.swarm_reduce_advance(cfg, hp, ptr(self.slabs), ctypes_ref(self.learner), self.capacity,
+                                            ptr(self.ctrl), stream_ptr()), "swarm_reduce_advance")
+        self.allreduce_grad()
 
     # ------------------------------------------------------------------ hipGraph
     def capture(self, n_ticks: int, fn=None):
@@ -231,6 +265,7 @@ class SwarmEngine:
 
     # ------------------------------------------------------------------ weights
     def state_dict(self) -> dict:
+        self.flush()
         return unflatten_params(self.params.detach().cpu())
 
     def load_state_dict(self, sd):

@@ -59,9 +59,13 @@ typedef struct swarm_ctrl {
   float eps;              /* exploration epsilon for the next tick                          */
   float loss;             /* last TD loss (0 when the update was skipped)                   */
   float grad_norm;        /* last pre-clip global gradient norm                             */
-  uint32_t trained;       /* 1 if the last TD step updated the weights                      */
+  uint32_t trained;       /* 1 = an optimizer step is pending (fused tick: applied by the next
+                             swarm_train_act_step or by swarm_adam_flush); 0 after swarm_adam_step */
   uint32_t episode;       /* episode counter (reset RNG key)                                */
-  uint32_t pad[7];
+  uint32_t pad0;
+  uint32_t beta_pow[4];   /* beta1^adam_step, beta2^adam_step as two little-endian doubles;
+                             initialise both to 1.0 (words 10-13)                          */
+  uint32_t pad[2];
 } swarm_ctrl;
 
 /* Replay ring (GraphReplayBuffer, train_gcn_dqn.py:25-48), SoA, per rank:
@@ -100,6 +104,22 @@ typedef struct swarm_adam_cfg {
   int32_t pad;
 } swarm_adam_cfg;
 
+/* Learner state for the fused training tick.  Weights/moments are ping-ponged so
+ * that every block of swarm_train_act_step can read the previous tick's values
+ * while block 0 persists the new ones: tick t reads *_cur, writes *_nxt;
+ * swarm_reduce_advance copies *_nxt back to *_cur.  All buffers hold N_PARAMS
+ * floats (grad: N_PARAMS + 1, the last = sum of squared TD errors). */
+typedef struct swarm_learner {
+  float* w_cur;
+  float* w_nxt;
+  float* m_cur;
+  float* m_nxt;
+  float* v_cur;
+  float* v_nxt;
+  float* target;
+  float* grad;
+} swarm_learner;
+
 int swarm_abi_version(void);
 int swarm_n_params(void);                 /* 1673 */
 const char* swarm_build_info(void);
@@ -137,6 +157,26 @@ int swarm_q_forward(const swarm_config* cfg, const float* params, const float* x
 int swarm_act_step(const swarm_config* cfg, const float* params, float* state,
                    const swarm_replay* replay, const swarm_ctrl* ctrl,
                    const swarm_act_out* out, void* stream);
+
+/* Fused training tick, acting half (train_gcn_dqn.py:161-172 + the optimizer step
+ * of the previous tick's TD loss, :125-133): if ctrl->trained, apply
+ * clip_grad_norm_ + Adam to (w_cur, grad) in every block (LDS image), block 0
+ * persists w_nxt/m_nxt/v_nxt (+ target sync); then act with w_nxt.
+ * Sequence per tick: swarm_train_act_step -> swarm_td_grad(params = w_nxt) ->
+ * swarm_reduce_advance [-> all-reduce(grad)]. */
+int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr,
+                         float* state, const swarm_replay* replay, const swarm_ctrl* ctrl,
+                         const swarm_act_out* out, void* stream);
+
+/* Slab sum -> lr->grad, copy *_nxt -> *_cur, record the pending update and
+ * advance ctrl (tick, replay slot). */
+int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
+                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
+
+/* Apply a pending update (ctrl->trained) to w_cur/m_cur/v_cur in place, e.g. after
+ * the last fused tick.  No tick advance. */
+int swarm_adam_flush(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr,
+                     swarm_ctrl* ctrl, void* stream);
 
 /* Acting-only rollout of n_ticks ticks with frozen weights in ONE launch
  * (Simulator.run_simulation, simulator.py:59-93, greedy when eps = 0).

@@ -447,31 +447,37 @@ def act_tick(params: dict, pos, vel, scenario: int, graph: int, k: int, eps: flo
 # ---------------------------------------------------------------------------
 # replay sampling (Feistel permutation; csrc swarm_sample_index)
 # ---------------------------------------------------------------------------
-def _feistel(x, bits, k0, k1, rnd):
-    """4-round alternating Feistel on (hi, lo) halves of a bits-wide word (bijective)."""
-    lo_bits = bits // 2
-    hi_bits = bits - lo_bits
-    lo_mask = (1 << lo_bits) - 1
-    hi_mask = (1 << hi_bits) - 1
-    L = x >> lo_bits
-    R = x & lo_mask
-    for r in range(4):
-        if r % 2 == 0:
-            w = philox.philox4x32(np.uint32(L), np.uint32(r), philox.STREAM_SAMPLE, np.uint32(rnd), k0, k1)[0]
-            R ^= int(w) & lo_mask
-        else:
-            w = philox.philox4x32(np.uint32(R), np.uint32(r), philox.STREAM_SAMPLE, np.uint32(rnd), k0, k1)[0]
-            L ^= int(w) & hi_mask
-    return (L << lo_bits) | R
+def _mix32(x: int) -> int:
+    """lowbias32 integer mixer (csrc swarm_common.h mix32)."""
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
 
 
 def sample_index(i: int, n: int, seed: int, rnd: int) -> int:
-    """i-th element of a keyed pseudo-random permutation of [0, n) (cycle walking)."""
-    bits = max(2, int(n - 1).bit_length())
+    """i-th element of a keyed pseudo-random permutation of [0, n): 4-round alternating
+    Feistel on a 2^bits domain, round function mix32(half ^ round_key), round keys =
+    one Philox block keyed by (seed, rnd); cycle walking back into [0, n)."""
     k0, k1 = philox.seed_key(seed)
+    rk = [int(w) for w in philox.philox4x32(np.uint32(rnd), 0, philox.STREAM_SAMPLE, 0, k0, k1)]
+    bits = 2
+    while bits < 32 and (1 << bits) < n:
+        bits += 1
+    lo_bits = bits // 2
+    hi_bits = bits - lo_bits
+    lo_mask, hi_mask = (1 << lo_bits) - 1, (1 << hi_bits) - 1
     x = i
     while True:
-        x = _feistel(x, bits, k0, k1, rnd)
+        L, R = x >> lo_bits, x & lo_mask
+        R ^= _mix32(L ^ rk[0]) & lo_mask
+        L ^= _mix32(R ^ rk[1]) & hi_mask
+        R ^= _mix32(L ^ rk[2]) & lo_mask
+        L ^= _mix32(R ^ rk[3]) & hi_mask
+        x = (L << lo_bits) | R
         if x < n:
             return x
 

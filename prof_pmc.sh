@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes (each in its own rocprofv3 run, kernel-trace only beside --pmc)
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/pmc}
+mkdir -p $OUT
+ARGS=${BENCH_ARGS:-"--steps 50 --warmup 5 --no-cpu-baseline --no-kernel-timing"}
+timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_MFMA SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- python bench.py $ARGS > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
+done

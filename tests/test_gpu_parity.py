@@ -282,7 +282,7 @@ def test_td_update_parity(sw, golden_weights, scen, N, S):
     eng.adam()
     torch.cuda.synchronize()
     c = eng.read_ctrl()
-    assert c["trained"] == 1 and c["adam_step"] == 1
+    assert c["trained"] == 0 and c["adam_step"] == 1
     assert abs(c["grad_norm"] - ref["total_norm"]) <= 1e-5 * max(1.0, ref["total_norm"])
     assert (eng.params.cpu() - ref["params"]).abs().max().item() < 2e-6
     assert_close_rel(eng.adam_v.cpu(), ref["v"], 1e-4, "adam v")
@@ -338,9 +338,13 @@ def test_td_skips_until_replay_holds_a_batch(sw):
         eng.train_tick()
         assert eng.read_ctrl()["trained"] == 0
     assert torch.equal(eng.params, p0)
-    eng.train_tick()               # 32 graphs
+    eng.train_tick()               # 32 graphs: fused tick leaves the optimizer step pending
     c = eng.read_ctrl()
-    assert c["trained"] == 1 and c["tick"] == 4 and c["filled_slots"] == 4
+    assert c["trained"] == 1 and c["tick"] == 4 and c["filled_slots"] == 4 and c["adam_step"] == 0
+    assert torch.equal(eng.params, p0)
+    eng.flush()
+    c = eng.read_ctrl()
+    assert c["trained"] == 0 and c["adam_step"] == 1
     assert not torch.equal(eng.params, p0)
 
 
@@ -355,6 +359,29 @@ def test_training_is_bitwise_deterministic(sw, golden_weights):
         torch.cuda.synchronize()
         outs.append((eng.params.clone(), eng.state.clone(), eng.read_ctrl()["loss"]))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]) and outs[0][2] == outs[1][2]
+
+
+@pytest.mark.parametrize("scen,N,graph", [("GoTo", 8, "complete"), ("ObstacleAvoidance", 12, "knn")])
+def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph):
+    """Fused tick (optimizer step deferred into the next act launch, ping-pong buffers)
+    == act + td_grad + grad_reduce + adam_step, bit for bit, incl. target syncs."""
+    p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 4)
+    kw = dict(seed=21, params=p, batch=48, eps=0.25, graph=graph, knn_k=5, update_target_every=3,
+              replay_capacity=16 * 64)
+    a = sw.SwarmEngine(scen, N, 16, **kw)
+    b = sw.SwarmEngine(scen, N, 16, **kw)
+    a.reset(0)
+    b.reset(0)
+    for _ in range(9):
+        a.train_tick()
+        b.train_tick_unfused()
+    a.flush()
+    torch.cuda.synchronize()
+    ca, cb = a.read_ctrl(), b.read_ctrl()
+    assert ca["adam_step"] == cb["adam_step"] == 7 and ca["tick"] == cb["tick"] == 9
+    assert torch.equal(a.params, b.params) and torch.equal(a.target, b.target)
+    assert torch.equal(a.adam_m, b.adam_m) and torch.equal(a.adam_v, b.adam_v)
+    assert torch.equal(a.state, b.state) and torch.equal(a.rep_s, b.rep_s)
 
 
 def test_graph_capture_replay_equals_eager(sw, golden_weights):
