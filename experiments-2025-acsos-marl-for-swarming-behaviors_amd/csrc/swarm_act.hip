@@ -5,6 +5,8 @@
 //   train_gcn_dqn.py:161-172   graph -> model -> eps-greedy -> env.step -> replay.push
 //   simulator.py:59-93         kNN graph -> argmax -> env.step -> metrics
 //   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:242-321
+#include <stdlib.h>
+
 #include "swarm_adam.h"
 #include "swarm_tile.h"
 
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(64 * kActTPB) void act_kernel(ActArgs A) {
       store4(A.lr.m_nxt, R.m, R.mt, tid);
       store4(A.lr.v_nxt, R.v, R.vt, tid);
       if (pending && (tnow % (uint32_t)A.hp.update_target_every) == 0u) store4(A.lr.target, R.w, R.wt, tid);
-      if (pending && tid == 0) *A.grad_norm_out = gn;
+      if (pending && tid == 0 && A.grad_norm_out) *A.grad_norm_out = gn;
     }
   } else if (MODE != MODE_STEP) {
     ParamStage<64 * kActTPB> ps;
@@ -413,7 +415,8 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
     return SWARM_E_BADARG;
   ActArgs a = make_args(cfg);
   a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp;
-  a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
+  static const bool no_gn = getenv("SWARM_NO_GN") != nullptr;   // A/B knob (diagnostics)
+  a.grad_norm_out = no_gn ? nullptr : const_cast<float*>(&ctrl->grad_norm);
   if (replay) a.replay = *replay;
   if (out) a.out = *out;
   return launch_act<MODE_TICK>(a, n_tiles(cfg), (hipStream_t)stream);

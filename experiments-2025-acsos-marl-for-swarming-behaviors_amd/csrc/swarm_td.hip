@@ -362,11 +362,16 @@ struct ReduceArgs {
   float beta1, beta2;
 };
 
-__global__ __launch_bounds__(256) void grad_reduce_kernel(ReduceArgs A) {
-  __shared__ float part[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+// 1024 threads = 64 columns x 16 slab groups; group g sums a contiguous run of at most
+// 16 slabs with every load issued before the ordered adds, then the 16 group sums are
+// added in group order (fixed order -> bitwise reproducible run to run).
+constexpr int kRedGroups = 16;
+__global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs A) {
+  __shared__ float part[kRedGroups][64];
+  const int c = threadIdx.x & 63;
+  const int col = blockIdx.x * 64 + c;
   const int q = threadIdx.x >> 6;
-  const int per = (A.n_slabs + 3) / 4;
+  const int per = (A.n_slabs + kRedGroups - 1) / kRedGroups;
   const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
   float s = 0.0f;
   if (col <= N_PARAMS) {
@@ -378,16 +383,17 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(ReduceArgs A) {
       for (int j = 0; j < 16; ++j) s = s + v[j];
     }
   }
-  if (A.advance && col < N_PARAMS) {   // ping-pong copy-back, one array per quarter
+  if (A.advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
     if (q == 0) A.lr.w_cur[col] = A.lr.w_nxt[col];
     else if (q == 1) A.lr.m_cur[col] = A.lr.m_nxt[col];
     else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
   }
-  part[q][threadIdx.x & 63] = s;
+  part[q][c] = s;
   __syncthreads();
   if (q == 0 && col <= N_PARAMS) {
-    const int c = threadIdx.x & 63;
-    const float tot = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
+    float tot = part[0][c];
+#pragma unroll
+    for (int gi = 1; gi < kRedGroups; ++gi) tot = tot + part[gi][c];
     A.grad[col] = tot;
     if (A.advance && col == N_PARAMS) {   // one thread: record the pending update, advance the tick
       swarm_ctrl* C = A.ctrl;
@@ -490,7 +496,7 @@ int td_tiles(const swarm_config* cfg, int batch) {
 int td_tpb_rt(int N) {
   static int env = [] { const char* e = getenv("SWARM_TD_TPB"); return e ? atoi(e) : 0; }();
   const int mx = N <= 16 ? 3 : 2;
-  int t = (env >= 1 && env <= 3) ? env : 2;
+  int t = (env >= 1 && env <= 3) ? env : 1;   // measured: 1 tile per block is fastest (256 blocks)
   return t < mx ? t : mx;
 }
 int td_blocks(const swarm_config* cfg, int batch) {
@@ -549,7 +555,7 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
   if (int e = check_td(cfg, hp)) return e;
   ReduceArgs a = {};
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = grad;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(64 * kRedGroups), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
@@ -562,7 +568,7 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
   a.beta1 = hp->beta1; a.beta2 = hp->beta2;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(64 * kRedGroups), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -58,7 +58,7 @@ def main():
     ab = (tiles + 3) // 4
     print(f"act_kernel ({ab} blocks x 4 waves):")
     report(sa.cpu().numpy()[: ab * 16 * 32].reshape(ab, 16, 32)[:, :4].reshape(-1), ACT, ab * 4)
-    tpb = int(os.environ.get("SWARM_TD_TPB", 2))
+    tpb = int(os.environ.get("SWARM_TD_TPB", 1))
     blocks = (tiles + tpb - 1) // tpb
     td = st.cpu().numpy()[: blocks * 16 * 32].reshape(blocks, 16, 32)
     print(f"td_kernel ({blocks} blocks x {tpb} tiles), online waves:")
