@@ -69,7 +69,9 @@ _PROTOS = {
     "swarm_train_act_step": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
                                        POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p]),
     "swarm_reduce_advance": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p, POINTER(SwarmLearner),
-                                       c_int32, c_void_p, c_void_p]),
+                                       c_int32, c_void_p, c_void_p, c_void_p]),
+    "swarm_sample_prepare": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_int32, c_void_p, c_void_p,
+                                       c_void_p]),
     "swarm_adam_flush": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
                                    c_void_p]),
     "swarm_rollout": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, c_int32, c_uint32, c_float,

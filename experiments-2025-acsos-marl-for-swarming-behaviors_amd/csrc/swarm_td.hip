@@ -360,6 +360,8 @@ struct ReduceArgs {
   swarm_ctrl* ctrl;
   int capacity, B, N, batch;
   float beta1, beta2;
+  int32_t* sample_next;   // fused tick: replay indices of the NEXT tick's TD batch
+  uint32_t k0, k1;        // sampling key (seed ^ rank salt)
 };
 
 // 1024 threads = 64 columns x 16 slab groups; group g sums a contiguous run of at most
@@ -389,7 +391,23 @@ __global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs
     else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
   }
   part[q][c] = s;
+  // the block holding column N_PARAMS also owns the control block: it reads ctrl
+  // before its single writer updates it, and draws the next tick's sample indices
+  // (the permutation the TD kernel would otherwise compute on its critical path)
+  const bool owner = A.advance && (blockIdx.x == (N_PARAMS / 64));
+  uint32_t c_tick = 0, c_filled = 0;
+  if (owner) { c_tick = A.ctrl->tick; c_filled = A.ctrl->filled_slots; }
   __syncthreads();
+  if (owner && A.sample_next) {
+    const uint32_t cap = (uint32_t)A.capacity;
+    const uint32_t f1 = c_filled + 1 < cap ? c_filled + 1 : cap;           // filled after this tick
+    const uint32_t vs = f1 + 1 < cap ? f1 + 1 : cap;                        // valid slots next tick
+    const uint32_t ng = vs * (uint32_t)A.B;
+    if (ng >= (uint32_t)A.batch) {
+      const SampleKey sk = sample_key(ng, A.k0, A.k1, c_tick + 1);
+      for (int i = threadIdx.x; i < A.batch; i += blockDim.x) A.sample_next[i] = (int32_t)sample_index((uint32_t)i, sk);
+    }
+  }
   if (q == 0 && col <= N_PARAMS) {
     float tot = part[0][c];
 #pragma unroll
@@ -560,7 +578,7 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
 }
 
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
-                         int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
+                         int32_t replay_capacity, swarm_ctrl* ctrl, int32_t* sample_next, void* stream) {
   if (int e = check_td(cfg, hp)) return e;
   if (!lr || !ctrl || replay_capacity < 1) return SWARM_E_BADARG;
   ReduceArgs a = {};
@@ -568,6 +586,9 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
   a.beta1 = hp->beta1; a.beta2 = hp->beta2;
+  a.sample_next = sample_next;
+  a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
+  a.k1 = (uint32_t)(cfg->seed >> 32);
   hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(64 * kRedGroups), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
@@ -578,6 +599,28 @@ static int launch_adam(const swarm_config* cfg, const swarm_adam_cfg* hp, float*
   a.hp = *hp; a.B = cfg->n_envs; a.N = cfg->n_agents; a.capacity = cap; a.flush = flush;
   a.params = params; a.target = target; a.m = m; a.v = v; a.grad = grad; a.ctrl = ctrl;
   hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(kAdamNT), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+__global__ void sample_prepare_kernel(const swarm_ctrl* C, int capacity, int B, int batch, uint32_t k0, uint32_t k1,
+                                      int32_t* out) {
+  const uint32_t cap = (uint32_t)capacity;
+  const uint32_t filled = C->filled_slots;
+  const uint32_t vs = filled + 1 < cap ? filled + 1 : cap;
+  const uint32_t ng = vs * (uint32_t)B;
+  if (ng < (uint32_t)batch) return;
+  const SampleKey sk = sample_key(ng, k0, k1, C->tick);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < batch; i += gridDim.x * blockDim.x)
+    out[i] = (int32_t)sample_index((uint32_t)i, sk);
+}
+
+int swarm_sample_prepare(const swarm_config* cfg, const swarm_adam_cfg* hp, int32_t replay_capacity,
+                         const swarm_ctrl* ctrl, int32_t* samples, void* stream) {
+  if (int e = check_td(cfg, hp)) return e;
+  if (!ctrl || !samples || replay_capacity < 1) return SWARM_E_BADARG;
+  const uint32_t k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
+  hipLaunchKernelGGL(sample_prepare_kernel, dim3((hp->batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, ctrl,
+                     replay_capacity, cfg->n_envs, hp->batch, k0, (uint32_t)(cfg->seed >> 32), samples);
   return (int)hipGetLastError();
 }
 

@@ -137,6 +137,8 @@ class SwarmEngine:
         self.slabs = torch.zeros(int(ws), **f32)
         self.grad = torch.zeros(N_PARAMS + 3, **f32)
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
+        self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
+        self._samples_valid = False   # fused path: indices for the next TD batch are ready
         # per-tick outputs
         self.q = torch.zeros(n_envs, n_agents, 9, **f32)
         self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
@@ -149,6 +151,10 @@ class SwarmEngine:
         self.out_min = SwarmActOut(0, 0, ptr(self.reward), 0, ptr(self.avg_dist), ptr(self.hits), 0, 0, 0, 0)
 
     # ------------------------------------------------------------------ control block
+    def invalidate(self):
+        """Call after editing ctrl / the replay by hand: the fused tick re-draws its samples."""
+        self._samples_valid = False
+
     def set_eps(self, eps: float):
         self.ctrl.view(torch.float32)[CTRL["eps"]].fill_(float(eps))
 
@@ -176,12 +182,14 @@ class SwarmEngine:
 
     # ------------------------------------------------------------------ acting
     def act(self, push: bool = True, full_out: bool = True):
+        self._samples_valid = False
         check(self.lib.swarm_act_step(ctypes_ref(self.cfg), ptr(self.params), ptr(self.state),
                                       ctypes_ref(self.replay) if push else None, ptr(self.ctrl),
                                       ctypes_ref(self.out if full_out else self.out_min), stream_ptr()),
               "swarm_act_step")
 
     def advance(self):
+        self._samples_valid = False
         check(self.lib.swarm_ctrl_advance(ctypes_ref(self.cfg), ctypes_ref(self.replay), ptr(self.ctrl),
                                           stream_ptr()), "swarm_ctrl_advance")
 
@@ -227,6 +235,7 @@ class SwarmEngine:
 
     def td_update(self, sample_in=None, sample_out=None):
         """Unfused TD update (API path): applies the optimizer step immediately."""
+        self._samples_valid = False
         self.flush()
         self.td_grad(sample_in, sample_out)
         self.allreduce_grad()
@@ -239,14 +248,19 @@ class SwarmEngine:
     def train_tick(self, full_out: bool = False):
         """Fused training tick: 3 launches (+ an RCCL all-reduce when world_size > 1)."""
         cfg, hp = ctypes_ref(self.cfg), ctypes_ref(self.hp)
+        if not self._samples_valid:
+            check(self.lib.swarm_sample_prepare(cfg, hp, self.capacity, ptr(self.ctrl), ptr(self.samples),
+                                                stream_ptr()), "swarm_sample_prepare")
         check(self.lib.swarm_train_act_step(cfg, hp, ctypes_ref(self.learner), ptr(self.state),
                                             ctypes_ref(self.replay), ptr(self.ctrl),
                                             ctypes_ref(self.out if full_out else self.out_min), stream_ptr()),
               "swarm_train_act_step")
         check(self.lib.swarm_td_grad(cfg, hp, ptr(self.w_nxt), ptr(self.target), ctypes_ref(self.replay),
-                                     ptr(self.ctrl), None, None, ptr(self.slabs), stream_ptr()), "swarm_td_grad")
+                                     ptr(self.ctrl), ptr(self.samples), None, ptr(self.slabs), stream_ptr()),
+              "swarm_td_grad")
         check(self.lib.swarm_reduce_advance(cfg, hp, ptr(self.slabs), ctypes_ref(self.learner), self.capacity,
-                                            ptr(self.ctrl), stream_ptr()), "swarm_reduce_advance")
+                                            ptr(self.ctrl), ptr(self.samples), stream_ptr()), "swarm_reduce_advance")
+        self._samples_valid = True
         self.allreduce_grad()
 
     # ------------------------------------------------------------------ hipGraph

@@ -169,9 +169,17 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
                          const swarm_act_out* out, void* stream);
 
 /* Slab sum -> lr->grad, copy *_nxt -> *_cur, record the pending update and
- * advance ctrl (tick, replay slot). */
+ * advance ctrl (tick, replay slot).  If sample_next != NULL it also draws the
+ * replay indices [batch] of the next tick's TD batch (pass them to swarm_td_grad
+ * as sample_in: identical to the in-kernel draw, off the TD critical path). */
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
-                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
+                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
+                         int32_t* sample_next, void* stream);
+
+/* Draw the TD batch's replay indices [batch] for the tick ctrl describes
+ * (GraphReplayBuffer.sample, train_gcn_dqn.py:40: keyed permutation, distinct ids). */
+int swarm_sample_prepare(const swarm_config* cfg, const swarm_adam_cfg* hp, int32_t replay_capacity,
+                         const swarm_ctrl* ctrl, int32_t* samples, void* stream);
 
 /* Apply a pending update (ctrl->trained) to w_cur/m_cur/v_cur in place, e.g. after
  * the last fused tick.  No tick advance. */
