@@ -78,13 +78,9 @@ def main():
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        pg = dist.group.WORLD
-
     import swarm_amd
+    from swarm_amd import dist as swdist
+    pg = swdist.init_process_group("nccl", local_rank) if world > 1 else None
     from swarm_amd import build as swbuild
     if rank == 0 and not swbuild.up_to_date():
         swbuild.build()
@@ -92,11 +88,12 @@ def main():
         torch.distributed.barrier()
 
     B, N = args.envs, args.agents
+    shard = swdist.Shard(rank, world, B)
     S = args.batch or B
     scen = args.scenario
     wkey = "weights_go_to" if scen == "GoTo" else "weights_obstacle_avoidance"
     w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
-    eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=rank * B,
+    eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=shard.env_offset,
                                 world_size=world, process_group=pg, update_target_every=200,
                                 replay_capacity=1_000_000)
     max_steps = 100

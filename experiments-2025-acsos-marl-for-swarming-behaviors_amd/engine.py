@@ -26,6 +26,7 @@ from typing import Optional
 import torch
 
 from . import _lib
+from .dist import allreduce_grad_
 from ._lib import (CTRL, N_PARAMS, SwarmActOut, SwarmAdamCfg, SwarmConfig, SwarmLearner, SwarmReplay, check, ptr,
                    stream_ptr)
 
@@ -219,9 +220,7 @@ class SwarmEngine:
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
     def allreduce_grad(self):
-        if self.world_size > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.process_group)
+        allreduce_grad_(self.grad, self.world_size, self.process_group)
 
     def adam(self):
         check(self.lib.swarm_adam_step(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.params), ptr(self.target),

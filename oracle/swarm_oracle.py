@@ -196,11 +196,14 @@ def grid_positions(centres: torch.Tensor, n_agents: int) -> torch.Tensor:
     return centres.to(torch.float32)[:, None, :] + offs[None, :, :]
 
 
-def reset_centres(scenario: int, n_envs: int, seed: int, episode: int, shared: bool, random_oa: bool = True):
+def reset_centres(scenario: int, n_envs: int, seed: int, episode: int, shared: bool, random_oa: bool = True,
+                  env_offset: int = 0):
     """Reset centres with Philox + Box-Muller in float64 (the HIP reset kernel uses
-    fp32 libm calls, so reset positions are compared with a tolerance)."""
+    fp32 libm calls, so reset positions are compared with a tolerance).  Draws are
+    keyed by the GLOBAL env index env_offset + e (rank sharding)."""
     k0, k1 = philox.seed_key(seed)
-    envs = np.zeros(n_envs, dtype=np.uint32) if shared else np.arange(n_envs, dtype=np.uint32)
+    envs = (np.zeros(n_envs, dtype=np.uint32) if shared
+            else np.arange(n_envs, dtype=np.uint32) + np.uint32(env_offset))
     w = philox.philox4x32(np.uint32(episode), envs, philox.STREAM_RESET, 0, k0, k1)
     u1 = ((w[0] >> np.uint32(8)).astype(np.float64) + 1.0) * 2.0 ** -24
     u2 = (w[1] >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
@@ -491,13 +494,12 @@ def complete_batch_edge_index(S: int, N: int) -> torch.Tensor:
     return torch.cat([base + s * N for s in range(S)], dim=1)
 
 
-def td_step(flat_params, flat_target, adam_m, adam_v, adam_step: int,
-            s_state, actions, rewards, s_next_state, gamma=0.99, lr=1e-3,
-            betas=(0.9, 0.999), eps=1e-8, max_norm=1.0, edge_index=None, edge_index_next=None):
-    """One DQN update on S sampled graphs of N nodes.
+def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma=0.99,
+                 edge_index=None, edge_index_next=None):
+    """TD loss and its gradient (train_gcn_dqn.py:113-124) on S sampled graphs of N nodes.
 
     s_state / s_next_state: [S,N,4] (pos, vel); actions [S,N] int; rewards [S,N].
-    Returns dict(loss, grad (pre-clip), total_norm, params, m, v, step).
+    Returns (loss, flat grad [N_PARAMS], online Q at the taken actions, TD targets).
     """
     S, N, _ = s_state.shape
     params = {k: v.clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
@@ -513,9 +515,21 @@ def td_step(flat_params, flat_target, adam_m, adam_v, adam_step: int,
         next_values = q_forward_edges(tparams, xn, ein).max(dim=1)[0]
     target = r + gamma * next_values
     loss = torch.nn.MSELoss()(values, target.unsqueeze(1))
-    plist = [params[k] for k, _ in PARAM_ORDER]
     loss.backward()
-    grad = torch.cat([p.grad.reshape(-1) for p in plist]).clone()
+    grad = torch.cat([params[k].grad.reshape(-1) for k, _ in PARAM_ORDER]).clone()
+    return float(loss.item()), grad, values.detach().squeeze(1), target
+
+
+def clip_adam(flat_params, grad, adam_m, adam_v, adam_step: int, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+              max_norm=1.0):
+    """clip_grad_norm_(params, max_norm) + torch.optim.Adam step (train_gcn_dqn.py:85,125-126)
+    with the gradient `grad` already in place.  Returns (params, m, v, total_norm)."""
+    plist = [v.clone().requires_grad_(True) for v in unflatten_params(flat_params).values()]
+    o = 0
+    for p in plist:
+        n = p.numel()
+        p.grad = torch.as_tensor(grad[o:o + n], dtype=torch.float32).reshape(p.shape).clone()
+        o += n
     total_norm = torch.nn.utils.clip_grad_norm_(plist, max_norm)
     opt = torch.optim.Adam(plist, lr=lr, betas=betas, eps=eps, foreach=False)
     if adam_step > 0:
@@ -535,5 +549,18 @@ def td_step(flat_params, flat_target, adam_m, adam_v, adam_step: int,
     m = torch.cat([st[i]["exp_avg"].reshape(-1) for i in range(len(plist))])
     v = torch.cat([st[i]["exp_avg_sq"].reshape(-1) for i in range(len(plist))])
     newp = torch.cat([p.detach().reshape(-1) for p in plist])
-    return dict(loss=float(loss.item()), grad=grad, total_norm=float(total_norm), params=newp,
-                m=m, v=v, step=adam_step + 1, values=values.detach().squeeze(1), target=target)
+    return newp, m, v, float(total_norm)
+
+
+def td_step(flat_params, flat_target, adam_m, adam_v, adam_step: int,
+            s_state, actions, rewards, s_next_state, gamma=0.99, lr=1e-3,
+            betas=(0.9, 0.999), eps=1e-8, max_norm=1.0, edge_index=None, edge_index_next=None):
+    """One DQN update (train_gcn_dqn.py:112-137): td_loss_grad + clip_adam.
+
+    Returns dict(loss, grad (pre-clip), total_norm, params, m, v, step, values, target).
+    """
+    loss, grad, values, target = td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_state,
+                                              gamma, edge_index, edge_index_next)
+    newp, m, v, total_norm = clip_adam(flat_params, grad, adam_m, adam_v, adam_step, lr, betas, eps, max_norm)
+    return dict(loss=loss, grad=grad, total_norm=total_norm, params=newp,
+                m=m, v=v, step=adam_step + 1, values=values, target=target)
