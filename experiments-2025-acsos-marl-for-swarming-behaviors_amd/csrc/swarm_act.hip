@@ -8,7 +8,8 @@
 #include <stdlib.h>
 
 #include "swarm_adam.h"
-#include "swarm_tile.h"
+#include "swarm_env.h"
+#include "swarm_wpg.h"
 
 namespace swarm {
 
@@ -34,37 +35,38 @@ struct ActArgs {
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
 };
 
-constexpr int kActTPB = 4;   // tiles (waves) per act block: weights staged / Adam applied once per 4 tiles
+constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
 
-template <int NMAX, int MODE>
-__global__ __launch_bounds__(64 * kActTPB) void act_kernel(ActArgs A) {
-  __shared__ WaveLds LW[kActTPB];
-  __shared__ __attribute__((aligned(16))) float Pw[N_PARAMS_PAD];
-  __shared__ float red[8 * kActTPB + 8];
+// One wave per environment (swarm_wpg.h).  Block-wide work is only the weight image
+// (LDS) — staged from global memory or produced by the fused Adam prologue.
+template <int NS, int MODE>
+__global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
+  __shared__ WScratch<NS> SW[kActWPB];
+  __shared__ __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
+  __shared__ float red[8 * kActWPB + 8];
   SWARM_STAMP(0);
-  WaveLds& L = LW[threadIdx.x >> 6];
-  const Geom g = make_geom(blockIdx.x * kActTPB + (threadIdx.x >> 6), A.N, A.B);
+  const int w = threadIdx.x >> 6;
   const int N = A.N;
-  const size_t node = g.valid ? (size_t)g.env * N + g.agent : 0;
+  const WGeom<NS> g = make_wgeom<NS>(blockIdx.x * kActWPB + w, A.B, N);
+  const WView<NS> V = SW[w].view();
+  WSmall<NS>& sm = SW[w].sm;
+  const int agent = g.valid ? g.s : 0;                 // idle slots alias agent 0: in-bounds reads, no writes
+  const size_t node = (size_t)g.gid * N + agent;
+  const bool writer = g.valid && g.q == 0;             // one lane per node slot stores
 
   // prologue: every independent global load in flight at once
-  FwdState F;
+  WFwd<NS> F;
   float px = 0.f, py = 0.f, vx = 0.f, vy = 0.f;
   if (MODE == MODE_Q) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) F.x[k] = k < kFeat ? A.x[node * kFeat + k] : 0.0f;
-    if (!g.valid) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
-    }
-    px = F.x[0]; py = F.x[1];
+    for (int k = 0; k < 8; ++k) F.x[k] = (k < kFeat && g.valid) ? A.x[node * kFeat + k] : 0.0f;
   } else {
     const float4 st = *reinterpret_cast<const float4*>(A.state + node * 4);
     if (g.valid) { px = st.x; py = st.y; vx = st.z; vy = st.w; }
   }
   if (MODE == MODE_TICK && A.learn) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
-    static_assert(64 * kActTPB == kAdamNT, "the act block is one Adam workgroup");
+    static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
     const int tid = threadIdx.x;
     AdamRegs R;
     R.load(A.lr.grad, A.lr.w_cur, A.lr.m_cur, A.lr.v_cur, tid);
@@ -83,11 +85,13 @@ __global__ __launch_bounds__(64 * kActTPB) void act_kernel(ActArgs A) {
       if (pending && tid == 0 && A.grad_norm_out) *A.grad_norm_out = gn;
     }
   } else if (MODE != MODE_STEP) {
-    ParamStage<64 * kActTPB> ps;
+    ParamStage<64 * kActWPB> ps;
     ps.load(A.params, threadIdx.x);
     ps.store(Pw, threadIdx.x);
   }
+  __syncthreads();   // weight image complete
   const float* P = Pw;
+  SWARM_STAMP(1);
 
   uint32_t tick = A.tick0;
   float eps = A.eps;
@@ -103,116 +107,122 @@ __global__ __launch_bounds__(64 * kActTPB) void act_kernel(ActArgs A) {
   for (int it = 0; it < n_ticks; ++it) {
     if (MODE != MODE_Q) {
       F.x[0] = px; F.x[1] = py; F.x[2] = vx; F.x[3] = vy;
-      F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)g.agent; F.x[7] = 0.0f;
+      F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)agent; F.x[7] = 0.0f;
       if (!g.valid) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
       }
     }
-    if (g.h == 0) { L.px[g.v] = px; L.py[g.v] = py; }
-    __syncthreads();
-    if (it == 0) SWARM_STAMP(1);
-    int mult[NMAX];
-    float c[NMAX];
-    if (MODE != MODE_STEP) tile_forward<NMAX, 2>(P, g, N, A.graph, A.k, A.conv, A.dense, L, F, mult, c);
+    if (MODE != MODE_STEP) {
+      wpg_forward<NS, 8>(P, g, N, A.graph, A.k, A.conv, A.dense, V, F);
+    } else {
+      if (g.q == 0) { sm.px[g.s] = px; sm.py[g.s] = py; }
+      wave_lds_sync();
+    }
+    if (it == 0) SWARM_STAMP(2);
 
     if (MODE == MODE_Q) {
-      if (g.valid && g.h == 0) {
+      if (g.valid) {   // lanes of the slot store the Q row together (from LDS: no dynamic register index)
 #pragma unroll
-        for (int a = 0; a < kActions; ++a) A.out.q[node * kActions + a] = F.q[a];
+        for (int j = 0; j < (kActions + Wpg<NS>::G - 1) / Wpg<NS>::G; ++j) {
+          const int a = g.q + j * Wpg<NS>::G;
+          if (a < kActions) A.out.q[node * kActions + a] = sm.Q[g.s][a];
+        }
       }
       return;
     }
 
     // ---- eps-greedy (train_gcn_dqn.py:164-167), one Philox coin per env and tick
     const uint32_t tk = tick + (uint32_t)it;
-    const uint32_t genv = (uint32_t)(A.env_offset + (g.valid ? g.env : 0));
+    const uint32_t genv = (uint32_t)(A.env_offset + g.gid);
     int action = (MODE == MODE_STEP) ? (g.valid ? A.actions[node] : 0) : argmax9(F.q);
     if (MODE != MODE_STEP && eps > 0.0f) {
       const float coin = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x);
       if (coin < eps) {   // the action draw only runs on exploring envs
-        const u32x4 w = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(g.agent >> 2), A.k0, A.k1);
-        const int j = g.agent & 3;
-        const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
+        const u32x4 wd = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
+        const int j = agent & 3;
+        const uint32_t word = j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w));
         action = uniform_int(word, kActions);
       }
     }
 
-    if (it == 0) SWARM_STAMP(8);
     // ---- env.step (VMAS World.step + scenario reward)
-    const StepOut o = agent_step<NMAX>(A.scenario, N, g.agent, px, py, vx, vy, action,
-                                       [&](int u, float& ux, float& uy) { ux = L.px[g.base + u]; uy = L.py[g.base + u]; });
-    if (it == 0) SWARM_STAMP(9);
-    if (g.h == 0) { L.red[g.v] = o.dgoal; L.red2[g.v] = (o.dobs <= 0.2f) ? 1.0f : 0.0f; }
-    __syncthreads();
-    float rew;
-    float dj[NMAX], hj[NMAX];
+    const StepOut o = agent_step<NS>(A.scenario, N, agent, px, py, vx, vy, action,
+                                     [&](int u, float& ux, float& uy) { ux = sm.px[u]; uy = sm.py[u]; });
+    if (it == 0) SWARM_STAMP(3);
+    if (g.q == 0) { sm.aux[g.s] = o.dgoal; sm.aux2[g.s] = (o.dobs <= 0.2f) ? 1.0f : 0.0f; }
+    wave_lds_sync();
+    float dj[NS], hj[NS];
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) { dj[j] = L.red[g.base + (j < N ? j : 0)]; hj[j] = L.red2[g.base + (j < N ? j : 0)]; }
+    for (int j = 0; j < NS; ++j) { dj[j] = sm.aux[j < N ? j : 0]; hj[j] = sm.aux2[j < N ? j : 0]; }
     float dsum = dj[0], hsum = hj[0];
 #pragma unroll
-    for (int j = 1; j < NMAX; ++j)
+    for (int j = 1; j < NS; ++j)
       if (j < N) { dsum = dsum + dj[j]; hsum = hsum + hj[j]; }
+    float rew;
     if (A.scenario == SWARM_GOTO) {
       rew = -dj[0];
 #pragma unroll
-      for (int j = 1; j < NMAX; ++j)
+      for (int j = 1; j < NS; ++j)
         if (j < N) rew = rew + (-dj[j]);   // go_to_position_scenario.py:112-113
     } else {
       rew = oa_reward(o.dgoal, o.dobs);
     }
     const float avg = dsum / (float)N;
     if (A.scenario == SWARM_GOTO) hsum = 0.0f;
-    if (it == 0) SWARM_STAMP(10);
 
-    if (g.valid && g.h == 0) {
-      if (MODE == MODE_TICK || MODE == MODE_STEP) {
-        if (MODE == MODE_TICK && A.out.q) {
+    if (MODE == MODE_TICK || MODE == MODE_STEP) {
+      if (MODE == MODE_TICK && A.out.q && g.valid) {
 #pragma unroll
-          for (int a = 0; a < kActions; ++a) A.out.q[node * kActions + a] = F.q[a];
+        for (int j = 0; j < (kActions + Wpg<NS>::G - 1) / Wpg<NS>::G; ++j) {
+          const int a = g.q + j * Wpg<NS>::G;
+          if (a < kActions) A.out.q[node * kActions + a] = sm.Q[g.s][a];
         }
+      }
+      if (writer) {
         if (A.out.actions) A.out.actions[node] = action;
         if (A.out.reward) A.out.reward[node] = rew;
         if (MODE == MODE_TICK && A.replay.s) {
-          const size_t ri = ((size_t)slot * A.B + g.env) * N + g.agent;
+          const size_t ri = ((size_t)slot * A.B + g.gid) * N + agent;
           reinterpret_cast<float4*>(A.replay.s)[ri] = make_float4(px, py, vx, vy);
           reinterpret_cast<float4*>(A.replay.s_next)[ri] = make_float4(o.px, o.py, o.vx, o.vy);
           A.replay.r[ri] = rew;
           A.replay.a[ri] = (uint8_t)action;
         }
-        if (MODE == MODE_TICK && A.out.mult && A.graph != SWARM_GRAPH_DENSE) {
-          for (int u = 0; u < N; ++u) A.out.mult[((size_t)g.env * N + u) * N + g.agent] = (uint8_t)mult[u];
+        if (agent == 0) {
+          if (A.out.avg_dist) A.out.avg_dist[g.gid] = avg;
+          if (A.out.hits) A.out.hits[g.gid] = hsum;
         }
-        if (g.agent == 0) {
-          if (A.out.avg_dist) A.out.avg_dist[g.env] = avg;
-          if (A.out.hits) A.out.hits[g.env] = hsum;
-        }
-      } else {  // MODE_ROLLOUT
-        if (A.out.traj_pos) {
-          const size_t ti = ((size_t)it * A.B + g.env) * N + g.agent;
-          reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o.px, o.py);
-        }
-        if (g.agent == 0) {
-          if (A.out.traj_dist) A.out.traj_dist[(size_t)it * A.B + g.env] = avg;
-          if (A.out.traj_hits) A.out.traj_hits[(size_t)it * A.B + g.env] = hsum;
-        }
+      }
+      if (MODE == MODE_TICK && A.out.mult && A.graph != SWARM_GRAPH_DENSE && g.valid) {
+        int mult[NS];
+        in_edges<NS>(g, N, A.graph, sm, nullptr, mult);
+        for (int u = g.q; u < N; u += Wpg<NS>::G) A.out.mult[((size_t)g.gid * N + u) * N + agent] = (uint8_t)mult[u];
+      }
+    } else if (writer) {  // MODE_ROLLOUT
+      if (A.out.traj_pos) {
+        const size_t ti = ((size_t)it * A.B + g.gid) * N + agent;
+        reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o.px, o.py);
+      }
+      if (agent == 0) {
+        if (A.out.traj_dist) A.out.traj_dist[(size_t)it * A.B + g.gid] = avg;
+        if (A.out.traj_hits) A.out.traj_hits[(size_t)it * A.B + g.gid] = hsum;
       }
     }
     rew_sum = rew_sum + rew;
     hits_sum = hits_sum + hsum;
     px = o.px; py = o.py; vx = o.vx; vy = o.vy;
-    if ((MODE == MODE_TICK || MODE == MODE_STEP) && g.valid && g.h == 0 && A.out.obs) {
+    if ((MODE == MODE_TICK || MODE == MODE_STEP) && writer && A.out.obs) {
       float* ob = A.out.obs + node * 6;
       ob[0] = px; ob[1] = py; ob[2] = vx; ob[3] = vy; ob[4] = kGoalX; ob[5] = kGoalY;
     }
-    if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && g.valid && g.h == 0 && g.agent == 0) {
-      if (A.out.avg_dist) A.out.avg_dist[g.env] = avg;
-      if (A.out.hits) A.out.hits[g.env] = hits_sum;
+    if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && writer && agent == 0) {
+      if (A.out.avg_dist) A.out.avg_dist[g.gid] = avg;
+      if (A.out.hits) A.out.hits[g.gid] = hits_sum;
     }
-    __syncthreads();
-    if (it == 0) SWARM_STAMP(11);
+    wave_lds_sync();   // every lane done with this tick's LDS rows before the next tick rewrites them
   }
-  if (g.valid && g.h == 0) {
+  if (writer) {
     reinterpret_cast<float4*>(A.state)[node] = make_float4(px, py, vx, vy);
     if (MODE == MODE_ROLLOUT) {
       if (A.out.reward) A.out.reward[node] = rew_sum;
@@ -222,7 +232,7 @@ __global__ __launch_bounds__(64 * kActTPB) void act_kernel(ActArgs A) {
       }
     }
   }
-  SWARM_STAMP(12);
+  SWARM_STAMP(4);
 }
 
 // ---------------------------------------------------------------- reset
@@ -257,26 +267,26 @@ __global__ void reset_kernel(int B, int N, int scenario, int flags, uint32_t k0,
 }
 
 // ---------------------------------------------------------------- graph build
-template <int NMAX>
+template <int NS>
 __global__ __launch_bounds__(64) void graph_kernel(ActArgs A, uint8_t* __restrict__ mult_out) {
-  __shared__ WaveLds L;
-  const Geom g = make_geom(blockIdx.x, A.N, A.B);
+  __shared__ WSmall<NS> sm;
   const int N = A.N;
-  const size_t node = g.valid ? (size_t)g.env * N + g.agent : 0;
-  if (g.h == 0) {
-    L.px[g.v] = g.valid ? A.x[node * kFeat + 0] : 0.0f;
-    L.py[g.v] = g.valid ? A.x[node * kFeat + 1] : 0.0f;
+  const WGeom<NS> g = make_wgeom<NS>(blockIdx.x, A.B, N);
+  const size_t node = (size_t)g.gid * N + (g.valid ? g.s : 0);
+  if (g.q == 0) {
+    sm.px[g.s] = g.valid ? A.x[node * kFeat + 0] : 0.0f;
+    sm.py[g.s] = g.valid ? A.x[node * kFeat + 1] : 0.0f;
   }
-  __syncthreads();
+  wave_lds_sync();
   if (A.graph == SWARM_GRAPH_KNN) {
-    const uint32_t m = g.valid ? knn_row<NMAX>(g, N, A.k, L) : 0u;
-    if (g.h == 0) L.knn[g.v] = m;
+    const uint32_t m = g.valid ? knn_mask<NS>(g, N, A.k, sm) : 0u;
+    if (g.q == 0) sm.knn[g.s] = m;
+    wave_lds_sync();
   }
-  __syncthreads();
-  int mult[NMAX];
-  graph_mult<NMAX>(g, N, A.graph, L, A.dense, mult);
-  if (g.valid && g.h == 0)
-    for (int u = 0; u < N; ++u) mult_out[((size_t)g.env * N + u) * N + g.agent] = (uint8_t)mult[u];
+  int mult[NS];
+  in_edges<NS>(g, N, A.graph, sm, nullptr, mult);
+  if (g.valid)
+    for (int u = g.q; u < N; u += Wpg<NS>::G) mult_out[((size_t)g.gid * N + u) * N + g.s] = (uint8_t)mult[u];
 }
 
 // ---------------------------------------------------------------- PyG edge list -> dense multiplicity
@@ -317,15 +327,12 @@ ActArgs make_args(const swarm_config* c) {
   return a;
 }
 
-int n_tiles(const swarm_config* c) {
-  const int E = kTile / c->n_agents;
-  return (c->n_envs + E - 1) / E;
-}
+int n_tiles(const swarm_config* c) { return c->n_envs; }   // one wave per environment
 
 template <int MODE>
 int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   if (tiles == 0) return 0;
-  const dim3 grid((tiles + kActTPB - 1) / kActTPB), block(64 * kActTPB);
+  const dim3 grid((tiles + kActWPB - 1) / kActWPB), block(64 * kActWPB);
   if (a.N <= 8) hipLaunchKernelGGL((act_kernel<8, MODE>), grid, block, 0, st, a);
   else if (a.N <= 16) hipLaunchKernelGGL((act_kernel<16, MODE>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((act_kernel<32, MODE>), grid, block, 0, st, a);
@@ -338,7 +345,7 @@ extern "C" {
 
 int swarm_abi_version(void) { return SWARM_ABI_VERSION; }
 int swarm_n_params(void) { return N_PARAMS; }
-const char* swarm_build_info(void) { return "libswarm_hip gfx950 (MFMA f32 32x32x2 tiles, wave64)"; }
+const char* swarm_build_info(void) { return "libswarm_hip gfx950 (wave-per-graph VALU forward, MFMA f32 32x32x2 weight-gradient products, wave64)"; }
 
 int swarm_env_reset(const swarm_config* cfg, float* state, uint32_t episode, void* stream) {
   if (int e = check_cfg(cfg)) return e;

@@ -143,10 +143,14 @@ __device__ inline void store4(float* __restrict__ dst, const float4* src, float 
   if (tid == 0) dst[N_PARAMS - 1] = tail;
 }
 
-// LDS weight image (N_PARAMS_PAD floats, pad zeroed)
+// padded LDS weight image (lds_index, N_LDS_PARAMS floats)
 __device__ inline void store_w_lds(float* __restrict__ lds, const AdamRegs& R, int tid) {
-  store4(lds, R.w, R.wt, tid);
-  if (tid == 0) { lds[N_PARAMS] = 0.0f; lds[N_PARAMS + 1] = 0.0f; lds[N_PARAMS + 2] = 0.0f; }
+#pragma unroll
+  for (int j = 0; j < kAdamNJ; ++j) {
+    const int i = tid + kAdamNT * j;
+    if (i < kAdamNF4) *reinterpret_cast<float4*>(lds + lds_index(4 * i)) = R.w[j];
+  }
+  if (tid == 0) lds[lds_index(N_PARAMS - 1)] = R.wt;
 }
 
 }  // namespace swarm

@@ -18,7 +18,6 @@ namespace swarm {
 constexpr int kHidden = 32;
 constexpr int kFeat = 7;
 constexpr int kActions = 9;
-constexpr int kTile = 32;            // node slots per wave (MFMA 32x32x2 f32 M/N)
 
 constexpr float kGoalX = -0.8f, kGoalY = 0.8f;      // go_to_position_scenario.py:86
 constexpr float kObstX = -0.1f, kObstY = 0.1f;      // obstacle_avoidance_scenario.py:247
@@ -40,8 +39,30 @@ constexpr int OFF_B1 = 1344;         // [32]
 constexpr int OFF_W2 = 1376;         // [9][32]
 constexpr int OFF_B2 = 1664;         // [9]
 constexpr int N_PARAMS = 1673;
-constexpr int N_PARAMS_PAD = 1676;   // 16-B multiple, LDS weight image
+constexpr int N_PARAMS_PAD = 1676;   // 16-B multiple (global buffers)
 static_assert(OFF_B2 + kActions == N_PARAMS, "param layout");
+
+// LDS weight image: the flat order with every lin1 / lin2 weight row padded to 36
+// floats, so MFMA fragment reads (16 rows x 4 columns per instruction) hit 64
+// distinct banks.  Float4 chunks of the flat vector never straddle a row.
+constexpr int kWRow = 36;
+constexpr int L_ATT_SRC = 0;
+constexpr int L_ATT_DST = 32;
+constexpr int L_BIAS = 64;
+constexpr int L_W = 96;
+constexpr int L_W1 = 320;                      // [32][36]
+constexpr int L_B1 = L_W1 + kHidden * kWRow;   // 1472
+constexpr int L_W2 = L_B1 + kHidden;           // 1504, [9][36]
+constexpr int L_B2 = L_W2 + kActions * kWRow;  // 1828
+constexpr int N_LDS_PARAMS = 1840;             // 16-B multiple
+__host__ __device__ constexpr int lds_index(int p) {
+  return p < OFF_W1 ? p
+       : p < OFF_B1 ? L_W1 + ((p - OFF_W1) >> 5) * kWRow + ((p - OFF_W1) & 31)
+       : p < OFF_W2 ? L_B1 + (p - OFF_B1)
+       : p < OFF_B2 ? L_W2 + ((p - OFF_W2) >> 5) * kWRow + ((p - OFF_W2) & 31)
+       : L_B2 + (p - OFF_B2);
+}
+static_assert(lds_index(N_PARAMS - 1) == L_B2 + kActions - 1 && L_B2 + kActions <= N_LDS_PARAMS, "LDS image");
 
 // RNG stream ids (third Philox counter word); must match oracle/philox.py
 constexpr uint32_t STREAM_COIN = 1;

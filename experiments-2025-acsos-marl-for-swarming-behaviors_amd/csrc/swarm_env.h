@@ -1,0 +1,68 @@
+// swarm_env.h — one agent's VMAS World.step + scenario reward, and argmax.
+//
+// VMAS 1.4.0 World.step restated; scenario rewards:
+// go_to_position_scenario.py:108-122, obstacle_avoidance_scenario.py:135-152.
+#pragma once
+#include "swarm_common.h"
+
+namespace swarm {
+
+struct StepOut {
+  float px, py, vx, vy;   // new state
+  float dgoal;            // distance to goal after the step
+  float dobs;             // World.get_distance(agent, obstacle) (OA)
+};
+
+// VMAS World.step for agent `agent` of an env whose pre-step positions are read
+// through pos(u).  Force order: 0 + u, obstacle pair, agent pairs in ascending
+// partner index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
+template <int NMAX, typename PosFn>
+__device__ inline StepOut agent_step(int scenario, int N, int agent, float px, float py, float vx, float vy,
+                                     int action, PosFn pos) {
+  float ux[NMAX], uy[NMAX];
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u) pos(u < N ? u : 0, ux[u], uy[u]);   // all reads issued first
+  float fx = 0.0f + action_level(action / 3);
+  float fy = 0.0f + action_level(action % 3);
+  if (scenario == SWARM_OBSTACLE_AVOIDANCE) {
+    float gx, gy;
+    pair_force(px - kObstX, py - kObstY, gx, gy);
+    fx = fx + gx; fy = fy + gy;
+  }
+#pragma unroll
+  for (int u = 0; u < NMAX; ++u) {
+    if (u < N) {
+      float gx, gy;
+      pair_force(px - ux[u], py - uy[u], gx, gy);   // u == agent: dist 0 < 1e-6 -> exactly 0
+      fx = fx + gx; fy = fy + gy;
+    }
+  }
+  StepOut o;
+  o.vx = vx * kDragKeep;
+  o.vy = vy * kDragKeep;
+  o.vx = o.vx + (fx / 1.0f) * kDt;
+  o.vy = o.vy + (fy / 1.0f) * kDt;
+  o.px = px + o.vx * kDt;
+  o.py = py + o.vy * kDt;
+  o.dgoal = norm2(o.px - kGoalX, o.py - kGoalY);
+  o.dobs = (norm2(o.px - kObstX, o.py - kObstY) - kRadius) - kRadius;
+  return o;
+}
+
+// OA per-agent reward (obstacle_avoidance_scenario.py:146-152)
+__device__ inline float oa_reward(float dgoal, float dobs) {
+  const float obst = dobs <= 1.0f ? -(1.0f - dobs) : 0.0f;
+  return -dgoal + 2.5f * obst;
+}
+
+// torch.argmax: first index of the maximum (train_gcn_dqn.py:168, simulator.py:64)
+__device__ inline int argmax9(const float q[kActions]) {
+  int best = 0;
+  float bv = q[0];
+#pragma unroll
+  for (int a = 1; a < kActions; ++a)
+    if (q[a] > bv) { bv = q[a]; best = a; }
+  return best;
+}
+
+}  // namespace swarm

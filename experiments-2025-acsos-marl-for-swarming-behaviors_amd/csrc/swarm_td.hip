@@ -5,44 +5,48 @@
 // Reference: DQNTrainer.train_step_dqn (src/training/train_gcn_dqn.py:112-137),
 // GraphReplayBuffer.sample (:38-45), Adam(lr=1e-3) (:85), target sync (:131-133).
 //
-// One wave per tile of E = 32/N sampled graphs.  Backward per tile:
+// Layout (swarm_wpg.h): one wave per sampled graph; a block holds 32 node slots.
+// Backward per graph (online wave, per-node vectors in registers):
 //   dQ[a] = (Q[a]-y) * 2/M                      (MSELoss mean, gather)
-//   dR = W2[a]^T dQ ; dZ = dR * [Z>0] ; dT = W1^T dZ (MFMA) ; dOut = dT * (1 - t^2)
+//   dR = W2[a]^T dQ ; dZ = dR * [Z>0] ; dT = W1^T dZ ; dOut = dT * (1 - t^2)
 //   GAT: g_uv = dOut_v.h_u ; de_uv = c_uv (g_uv - sum_w c_wv g_wv) ; dp = de * leaky'(p)
 //        da_dst[v] = sum_u dp_uv ; da_src[u] = sum_v dp_uv ; dh_u = sum_v c_uv dOut_v + da_src att_src + da_dst att_dst
-//   parameter sums over the tile's nodes: dW1 = dZ^T T, dW2 = dQ^T R, dW = dh^T X on MFMA
-//   (32x32x2 f32, node index as K), vectors by LDS column sums.
-// Each block writes one slab [N_PARAMS + 1] (last = sum of squared TD errors);
-// swarm_grad_reduce sums slabs in a fixed order (bitwise run-to-run reproducible).
+// Parameter sums over the block's 32 node rows: dW1 = dZ^T T, dW2 = dQ^T R, dW = dh^T X on
+// MFMA (32x32x2 f32, node index as K), vectors by LDS column sums; each block writes one
+// slab [N_PARAMS + 1] (last = sum of squared TD errors) and swarm_grad_reduce sums the
+// slabs in a fixed order (bitwise run-to-run reproducible).
 #include <stdlib.h>
 
 #include "swarm_adam.h"
-#include "swarm_tile.h"
+#include "swarm_wpg.h"
 
 namespace swarm {
 
-template <int NMAX>
-struct TdTileLds {
-  WaveLds L;                      // online forward scratch (H rows, scores, positions)
-  WaveLds LT;                     // target forward scratch
-  float T[kTile][kHsStride];      // tanh(conv out), natural order    } reused as this tile's
-  float R[kTile][kHsStride];      // relu(lin1)                        } partial slab after the
-  float dZ[kTile][kHsStride];     //                                   } parameter products
-  float dO[kTile][kHsStride];     // dL/d conv out
-  float dH[kTile][kHsStride];     // dL/d h
-  float X[kTile][9];              // features (k < 8)
-  float cm[kTile][NMAX + 1];      // c[target slot][source agent]
-  float dp[kTile][NMAX + 1];      // dp[target slot][source agent]
-  float y[kTile];                 // TD targets from the target wave
-  float gq[kTile];
-  float das[kTile], dad[kTile];
-  float d2[kTile];
-  int act[kTile];
-};
-static_assert(5 * kTile * kHsStride >= N_PARAMS + 1, "partial slab fits the image area");
+// One TD block = 32 node slots = GPB = 32 / NS sampled graphs.  Wave w < GPB runs the
+// ONLINE network on graph w (forward on s with activations kept, dQ, backward of the
+// per-node vectors); wave GPB + w runs the TARGET network on s' of graph w
+// (y = r + gamma max_a Q_tgt), then shares the parameter products.  The parameter
+// gradient of the block is a sum over its 32 node rows: MFMA 32x32x2 f32 with the
+// node index as K, jobs spread over the waves, each writing its slice of the slab.
+constexpr int kTdRows = 32;
 
-// tiles per block; each tile has an online wave and a target wave (2 * TPB waves)
-template <int NMAX> constexpr int td_tpb_max() { return NMAX <= 16 ? 3 : 2; }
+template <int NS>
+struct TdLds {
+  static constexpr int GPB = kTdRows / NS;
+  float H[kTdRows][kRow];         // online conv1.lin output
+  float T[kTdRows][kRow];         // tanh(conv out)
+  float R[kTdRows][kRow];         // relu(lin1)
+  float dZ[kTdRows][kRow];        // dL/d lin1 pre-activation
+  float dO[kTdRows][kRow];        // dL/d conv out
+  float dH[kTdRows][kRow];        // dL/d h
+  float X[kTdRows][9];            // node features (k < 8)
+  float cm[kTdRows][NS + 1];      // c[target row][source slot]
+  float dp[kTdRows][NS + 1];      // dL/d pre-activation of edge (source -> target row)
+  float y[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];
+  int act[kTdRows];
+  WSmall<NS> on[GPB];             // online waves' per-graph scratch
+  WScratch<NS> tg[GPB];           // target waves' forward scratch
+};
 
 struct TdArgs {
   int S, B, N, graph, k, conv, env_offset;
@@ -58,14 +62,8 @@ struct TdArgs {
   float grad_scale;   // fp32(2 / M_local)
 };
 
-__device__ inline void store_acc_row(float (*img)[kHsStride], int v, int h, const float val[16]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    *reinterpret_cast<float4*>(&img[v][8 * q + 4 * h]) = make_float4(val[4 * q], val[4 * q + 1], val[4 * q + 2], val[4 * q + 3]);
-}
-
-// D[i][j] = sum_node A_img[node][i] * B_img[node][j] over the 32 node slots (MFMA, K = node)
-__device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kHsStride], const float (*Bimg)[kHsStride], int lane) {
+// D[i][j] = sum_node A_img[node][i] * B_img[node][j] over the 32 node rows (MFMA, K = node)
+__device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*Bimg)[kRow], int lane) {
   f32x16 acc = {};
   const int h = lane >> 5, c = lane & 31;
 #pragma unroll
@@ -73,30 +71,27 @@ __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kHsStride], const floa
   return acc;
 }
 
-// Waves 0..TPB-1: online network of tile w (forward with activations kept, backward,
-// dW / att gradients); waves TPB..2TPB-1: target network of tile w-TPB (forward on s',
-// y = r + gamma max Q_tgt), then the dW1 / dW2 / bias products while the online wave
-// runs the GAT backward.  Every wave passes the same __syncthreads() sequence.
-template <int NMAX, int TPB>
-__global__ __launch_bounds__(128 * TPB) void td_kernel(TdArgs A) {
-  static_assert(TPB <= td_tpb_max<NMAX>(), "LDS budget");
-  __shared__ TdTileLds<NMAX> TW[TPB];
-  __shared__ __attribute__((aligned(16))) float Pon[N_PARAMS_PAD];
-  __shared__ __attribute__((aligned(16))) float Ptg[N_PARAMS_PAD];
+template <int NS>
+__global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
+  constexpr int GPB = kTdRows / NS, G = Wpg<NS>::G, FPL = Wpg<NS>::FPL;
+  constexpr int NT = 128 * GPB;
+  __shared__ TdLds<NS> TB;
+  __shared__ __attribute__((aligned(16))) float Pon[N_LDS_PARAMS];
+  __shared__ __attribute__((aligned(16))) float Ptg[N_LDS_PARAMS];
   const int wave = threadIdx.x >> 6;
-  const int tl = wave % TPB;
-  const bool online = wave < TPB;
-  TdTileLds<NMAX>& T = TW[tl];
-  WaveLds& L = online ? T.L : T.LT;
+  const bool online = wave < GPB;
+  const int wi = online ? wave : wave - GPB;
   const int N = A.N;
-  const Geom g = make_geom(blockIdx.x * TPB + tl, N, A.S);
-  const int lane = g.lane, h = g.h;
+  const WGeom<NS> g = make_wgeom<NS>(blockIdx.x * GPB + wi, A.S, N);
+  const int row0 = wi * NS, row = row0 + g.s;
+  const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
+  const int lane = g.lane;
+  const int agent = g.valid ? g.s : 0;
   float* gslab = A.slabs + (size_t)blockIdx.x * (N_PARAMS + 1);
-  float* slab = &T.T[0][0];       // this tile's partial slab (after the products)
   SWARM_STAMP(0);
 
   // ---- weights: both images' loads issued first (one round trip)
-  ParamStage<128 * TPB> pon, ptg;
+  ParamStage<NT> pon, ptg;
   pon.load(A.params, threadIdx.x);
   ptg.load(A.target, threadIdx.x);
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
@@ -105,247 +100,254 @@ __global__ __launch_bounds__(128 * TPB) void td_kernel(TdArgs A) {
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
   const uint32_t n_graphs = valid_slots * (uint32_t)A.B;
   if (n_graphs < (uint32_t)A.S) {
-    for (int p = threadIdx.x; p <= N_PARAMS; p += 128 * TPB) gslab[p] = 0.0f;
+    for (int p = threadIdx.x; p <= N_PARAMS; p += NT) gslab[p] = 0.0f;
     return;
   }
-  SWARM_STAMP(1);
   // ---- sample (GraphReplayBuffer.sample: random.sample -> keyed permutation)
   uint32_t gid = 0;
   if (A.sample_in) {
-    gid = (uint32_t)A.sample_in[g.valid ? g.env : 0];
+    gid = (uint32_t)A.sample_in[g.gid];
   } else {
     const SampleKey sk = sample_key(n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, A.ctrl->tick);
-    gid = sample_index((uint32_t)(g.valid ? g.env : 0), sk);
+    gid = sample_index((uint32_t)g.gid, sk);
   }
-  if (A.sample_out && online && g.valid && h == 0 && g.agent == 0) A.sample_out[g.env] = (int32_t)gid;
-  SWARM_STAMP(2);
+  if (A.sample_out && online && g.live && lane == 0) A.sample_out[g.gid] = (int32_t)gid;
+  SWARM_STAMP(1);
   const uint32_t slot = gid / (uint32_t)A.B, genv = gid % (uint32_t)A.B;
-  const size_t ri = ((size_t)slot * A.B + genv) * N + g.agent;
+  const size_t ri = ((size_t)slot * A.B + genv) * N + agent;
   const float4 st = reinterpret_cast<const float4*>(online ? A.replay.s : A.replay.s_next)[ri];
   const float rew = A.replay.r[ri];
   const int act = g.valid ? (int)A.replay.a[ri] : 0;
   pon.store(Pon, threadIdx.x);
   ptg.store(Ptg, threadIdx.x);
 
-  FwdState F;
+  WFwd<NS> F;
   F.x[0] = st.x; F.x[1] = st.y; F.x[2] = st.z; F.x[3] = st.w;
-  F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)g.agent; F.x[7] = 0.0f;
+  F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)agent; F.x[7] = 0.0f;
   if (!g.valid) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
   }
-  if (h == 0) { L.px[g.v] = F.x[0]; L.py[g.v] = F.x[1]; }
-  int mult[NMAX];
-  float c[NMAX];
-  __syncthreads();
-  SWARM_STAMP(3);
+  if (online && g.q == 0) TB.act[row] = act;
+  __syncthreads();   // B0: weight images
+  SWARM_STAMP(2);
   // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121)
-  tile_forward<NMAX, 16>(online ? Pon : Ptg, g, N, A.graph, A.k, A.conv, nullptr, L, F, mult, c);
-  if (!online) {
+  wpg_forward<NS, 16>(online ? Pon : Ptg, g, N, A.graph, A.k, A.conv, nullptr, V, F);
+  if (!online && g.q == 0) {
     float qmax = F.q[0];
 #pragma unroll
     for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[a]);
-    if (h == 0) T.y[g.v] = rew + A.gamma * qmax;
+    TB.y[row] = rew + A.gamma * qmax;
   }
+  SWARM_STAMP(3);
+  __syncthreads();   // B1: TD targets
   SWARM_STAMP(4);
-  __syncthreads();
-  SWARM_STAMP(5);
 
   const float* P = Pon;
-  float delta = 0.0f;
-  float dO[16];
+  constexpr int CT = Dl<NS>::CT;
+  const int c = lane & 15, p = lane >> 4;
+  float dz[CT][2][4];
   if (online) {
-    float qa = F.q[0];
+    // ---- dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ, dZ = dR * [z > 0]
+    //      in D layout: lane (c, p) handles node 16 ct + c, features 16 t + 4 p + r
 #pragma unroll
-    for (int a = 1; a < kActions; ++a) qa = (act == a) ? F.q[a] : qa;
-    delta = g.valid ? (qa - T.y[g.v]) : 0.0f;
-    const float gq = delta * A.grad_scale;
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c, nn = min(n, NS - 1);
+      const bool nv = g.live && n < N;
+      const int an = TB.act[row0 + nn];
+      const float delta = nv ? (V.sm->Q[nn][an] - TB.y[row0 + nn]) : 0.0f;
+      const float gq = delta * A.grad_scale;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float4 w = *reinterpret_cast<const float4*>(P + L_W2 + an * kWRow + 16 * t + 4 * p);
+        const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz[ct][t][r] = F.zr[ct][t][r] > 0.0f ? wv[r] * gq : 0.0f;
+      }
+      if (n < NS) {
+        *reinterpret_cast<float4*>(&TB.dZ[row0 + n][4 * p]) = make_float4(dz[ct][0][0], dz[ct][0][1], dz[ct][0][2], dz[ct][0][3]);
+        *reinterpret_cast<float4*>(&TB.dZ[row0 + n][16 + 4 * p]) = make_float4(dz[ct][1][0], dz[ct][1][1], dz[ct][1][2], dz[ct][1][3]);
+        if (p == 0) { TB.gq[row0 + n] = gq; TB.d2[row0 + n] = delta * delta; }
+      }
+    }
+    if (g.q == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) TB.X[row][k] = k < kFeat ? F.x[k] : 0.0f;
+      TB.X[row][8] = 0.0f;
+    }
     if (!g.valid) {
 #pragma unroll
-      for (int u = 0; u < NMAX; ++u) c[u] = 0.0f;
+      for (int u = 0; u < NS; ++u) F.c[u] = 0.0f;
     }
-    // ---- MLP backward
-    float dZ[16], dT[16];
-    {
-      float w2[16];
-      load_vec_acc(P + OFF_W2 + act * kHidden, h, w2);
+    if (g.q == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float dR = w2[r] * gq;
-        dZ[r] = F.zr[r] > 0.0f ? dR : 0.0f;
-      }
-    }
-    mfma_lin32_t(P + OFF_W1, g, dZ, dT);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dO[r] = dT[r] * (1.0f - F.t[r] * F.t[r]);
-    SWARM_STAMP(6);
-    store_acc_row(T.T, g.v, h, F.t);
-    store_acc_row(T.R, g.v, h, F.zr);
-    store_acc_row(T.dZ, g.v, h, dZ);
-    store_acc_row(T.dO, g.v, h, dO);
-    if (h == 0) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) T.X[g.v][k] = k < kFeat ? F.x[k] : 0.0f;
-      T.X[g.v][8] = 0.0f;
-      T.gq[g.v] = gq;
-      T.act[g.v] = act;
-      T.d2[g.v] = delta * delta;
-#pragma unroll
-      for (int u = 0; u < NMAX; ++u)
-        if (u < N) T.cm[g.v][u] = c[u];
+      for (int u = 0; u < NS; ++u) TB.cm[row][u] = F.c[u];
     }
   }
-  __syncthreads();   // images of every tile ready
-  SWARM_STAMP(7);
+  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph
+  SWARM_STAMP(5);
 
-  const int col = lane & 31;
-  // target-wave products (registers) while the online wave does the GAT backward
-  f32x16 dW1 = {}, dW2 = {};
-  float s_bias = 0.0f, s_b1 = 0.0f, s_b2 = 0.0f, s_loss = 0.0f;
-  float da_s = 0.0f, da_d = 0.0f;
-  if (!online) {
-    dW1 = mfma_nodesum(T.dZ, T.T, lane);                       // dW1[i][hid]
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {                             // dW2[a][hid]
-      const int n = 2 * s + h;
-      const float a = (T.act[n] == col) ? T.gq[n] : 0.0f;
-      dW2 = mfma32(a, T.R[n][col], dW2);
-    }
-    if (h == 0) {
-      for (int n = 0; n < kTile; ++n) s_bias = s_bias + T.dO[n][col];
-    } else {
-      for (int n = 0; n < kTile; ++n) s_b1 = s_b1 + T.dZ[n][col];
-    }
-    if (lane < kActions) {
-      for (int n = 0; n < kTile; ++n) s_b2 = s_b2 + (T.act[n] == lane ? T.gq[n] : 0.0f);
-    } else if (lane == 63) {
-      for (int n = 0; n < kTile; ++n) s_loss = s_loss + T.d2[n];
-    }
-  } else if (A.conv == SWARM_CONV_GAT) {
-    // ---- GAT backward (attention part), branch-free over the env's sources u
-    float gu[NMAX];
-#pragma unroll
-    for (int u = 0; u < NMAX; ++u) {
-      gu[u] = 0.0f;
-      if (u < N) {
-        const float* row = &L.hs[g.base + u][4 * h];
-        float p = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 hv = *reinterpret_cast<const float4*>(row + 8 * q);
-          p = p + dO[4 * q] * hv.x;
-          p = p + dO[4 * q + 1] * hv.y;
-          p = p + dO[4 * q + 2] * hv.z;
-          p = p + dO[4 * q + 3] * hv.w;
-        }
-        gu[u] = p;
-      }
-    }
-    float G = 0.0f;
-#pragma unroll
-    for (int u = 0; u < NMAX; ++u) {
-      if (u < N) gu[u] = gu[u] + xor32(gu[u]);
-      if (u < N) G = G + c[u] * gu[u];
-    }
-#pragma unroll
-    for (int u = 0; u < NMAX; ++u) {
-      float dpu = 0.0f;
-      if (u < N) {
-        const float de = c[u] * (gu[u] - G);
-        const float pre = L.ssrc[g.base + u] + F.sdst;
-        dpu = pre > 0.0f ? de : de * kLeakySlope;
-      }
-      da_d = da_d + dpu;
-      if (u < N && h == 0) T.dp[g.v][u] = dpu;
-    }
-  }
-  __syncthreads();   // dp ready
-  SWARM_STAMP(8);
+  const int col = lane & 31, h = lane >> 5;
   if (online) {
+    // ---- dT^T[feature][node] = W1^T dZ^T on MFMA (k-step (t, r) -> k = 16 t + 4 p + r,
+    //      the dz registers are the B operand), dO = dT * (1 - t^2), D layout
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c, nn = min(n, NS - 1);
+      const bool nv = g.live && n < N;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc = mfma16(P[L_W1 + (16 * t + 4 * p + r) * kWRow + 16 * t2 + c], dz[ct][t][r], acc);
+        const float4 tv = *reinterpret_cast<const float4*>(&TB.T[row0 + nn][16 * t2 + 4 * p]);
+        const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = nv ? acc[r] * (1.0f - tt[r] * tt[r]) : 0.0f;
+        if (n < NS) *reinterpret_cast<float4*>(&TB.dO[row0 + n][16 * t2 + 4 * p]) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    wave_lds_sync();   // dO rows of this graph
+    float dO[FPL];
+    lds_load<FPL>(&TB.dO[row][g.f0], dO);
+    // ---- GAT backward (attention part), branch-free over the graph's sources u
+    float da_d = 0.0f;
     if (A.conv == SWARM_CONV_GAT) {
-      float col_dp[NMAX];
+      float gu[NS];
 #pragma unroll
-      for (int w = 0; w < NMAX; ++w) col_dp[w] = T.dp[g.base + (w < N ? w : 0)][g.agent];
+      for (int u = 0; u < NS; ++u) {
+        gu[u] = 0.0f;
+        if (u < N) {
+          float hv[FPL];
+          lds_load<FPL>(&TB.H[row0 + u][g.f0], hv);
+          float part = 0.0f;
 #pragma unroll
-      for (int w = 0; w < NMAX; ++w)
-        if (w < N) da_s = da_s + col_dp[w];
+          for (int i = 0; i < FPL; ++i) part = part + dO[i] * hv[i];
+          gu[u] = slot_sum<G>(part);
+        }
+      }
+      float Gs = 0.0f;
+#pragma unroll
+      for (int u = 0; u < NS; ++u)
+        if (u < N) Gs = Gs + F.c[u] * gu[u];
+      WSmall<NS>& sm = *V.sm;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        float dpu = 0.0f;
+        if (u < N) {
+          const float de = F.c[u] * (gu[u] - Gs);
+          const float pre = sm.ssrc[u] + F.sdst;
+          dpu = pre > 0.0f ? de : de * kLeakySlope;
+        }
+        da_d = da_d + dpu;
+        if (u < N && g.q == 0) TB.dp[row][u] = dpu;
+      }
+    }
+    wave_lds_sync();   // dp rows of this graph
+    float da_s = 0.0f;
+    if (A.conv == SWARM_CONV_GAT) {
+#pragma unroll
+      for (int v = 0; v < NS; ++v)
+        if (v < N) da_s = da_s + TB.dp[row0 + v][agent];
     }
     if (!g.valid) { da_s = 0.0f; da_d = 0.0f; }
-    // ---- dh = messages + attention-coefficient terms
-    float dh[16];
-    float as[16], ad[16];
-    load_vec_acc(P + OFF_ATT_SRC, h, as);
-    load_vec_acc(P + OFF_ATT_DST, h, ad);
+    // ---- dh = sum_v c[v][me] dO_v + da_src att_src + da_dst att_dst
+    float dh[FPL], as[FPL], ad[FPL];
+    lds_load<FPL>(P + L_ATT_SRC + g.f0, as);
+    lds_load<FPL>(P + L_ATT_DST + g.f0, ad);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] = 0.0f;
+    for (int i = 0; i < FPL; ++i) dh[i] = 0.0f;
 #pragma unroll
-    for (int w = 0; w < NMAX; ++w) {
-      if (w < N) {
-        const float cw = g.valid ? T.cm[g.base + w][g.agent] : 0.0f;   // c[target w][source me]
-        const float* row = &T.dO[g.base + w][4 * h];
+    for (int v = 0; v < NS; ++v) {
+      if (v < N) {
+        const float cv = g.valid ? TB.cm[row0 + v][agent] : 0.0f;   // c[target v][source me]
+        float dv[FPL];
+        lds_load<FPL>(&TB.dO[row0 + v][g.f0], dv);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 dv = *reinterpret_cast<const float4*>(row + 8 * q);
-          dh[4 * q] = dh[4 * q] + cw * dv.x;
-          dh[4 * q + 1] = dh[4 * q + 1] + cw * dv.y;
-          dh[4 * q + 2] = dh[4 * q + 2] + cw * dv.z;
-          dh[4 * q + 3] = dh[4 * q + 3] + cw * dv.w;
-        }
+        for (int i = 0; i < FPL; ++i) dh[i] = dh[i] + cv * dv[i];
       }
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh[r] = (dh[r] + da_s * as[r]) + da_d * ad[r];
-    store_acc_row(T.dH, g.v, h, dh);
-    if (h == 0) { T.das[g.v] = da_s; T.dad[g.v] = da_d; }
-  }
-  __syncthreads();   // dH ready
-  SWARM_STAMP(9);
-  f32x16 dW = {};
-  float s_as = 0.0f, s_ad = 0.0f;
-  if (online) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {                             // dW[hid][k]
-      const int n = 2 * s + h;
-      dW = mfma32(T.dH[n][col], col < 8 ? T.X[n][col] : 0.0f, dW);
-    }
-    if (h == 0) {
-      for (int n = 0; n < kTile; ++n) s_as = s_as + T.das[n] * L.hs[n][col];
-    } else {
-      for (int n = 0; n < kTile; ++n) s_ad = s_ad + T.dad[n] * L.hs[n][col];
-    }
-  }
-  SWARM_STAMP(10);
-  __syncthreads();   // every image read done: the image area becomes the partial slab
-  if (online) {
-    if (col < kFeat) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) slab[OFF_W + acc_row(r, h) * kFeat + col] = dW[r];
-    }
-    if (h == 0) slab[OFF_ATT_SRC + col] = s_as;
-    else        slab[OFF_ATT_DST + col] = s_ad;
+    for (int i = 0; i < FPL; ++i) dh[i] = (dh[i] + da_s * as[i]) + da_d * ad[i];
+    lds_store<FPL>(&TB.dH[row][g.f0], dh);
+    if (g.q == 0) { TB.das[row] = da_s; TB.dad[row] = da_d; }
   } else {
+    // ---- target waves: products that need only B2's images
+    //      job 0: dW1 = dZ^T T ; job 1: dW2 = onehot(a) gq R, db2, loss ; job 2: db1
+    for (int job = wi; job < 3; job += GPB) {
+      if (job == 0) {
+        const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) slab[OFF_W1 + acc_row(r, h) * kHidden + col] = dW1[r];
+        for (int r = 0; r < 16; ++r) gslab[OFF_W1 + acc_row(r, h) * kHidden + col] = dW1[r];
+      } else if (job == 1) {
+        f32x16 dW2 = {};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int a = acc_row(r, h);
-      if (a < kActions) slab[OFF_W2 + a * kHidden + col] = dW2[r];
+        for (int s = 0; s < 16; ++s) {
+          const int n = 2 * s + h;
+          const float a = (TB.act[n] == col) ? TB.gq[n] : 0.0f;
+          dW2 = mfma32(a, TB.R[n][col], dW2);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int a = acc_row(r, h);
+          if (a < kActions) gslab[OFF_W2 + a * kHidden + col] = dW2[r];
+        }
+        if (lane < kActions) {
+          float s_b2 = 0.0f;
+          for (int n = 0; n < kTdRows; ++n) s_b2 = s_b2 + (TB.act[n] == lane ? TB.gq[n] : 0.0f);
+          gslab[OFF_B2 + lane] = s_b2;
+        } else if (lane == 63) {
+          float s_loss = 0.0f;
+          for (int n = 0; n < kTdRows; ++n) s_loss = s_loss + TB.d2[n];
+          gslab[N_PARAMS] = s_loss;
+        }
+      } else {
+        if (lane < kHidden) {
+          float s_b1 = 0.0f;
+          for (int n = 0; n < kTdRows; ++n) s_b1 = s_b1 + TB.dZ[n][lane];
+          gslab[OFF_B1 + lane] = s_b1;
+        }
+      }
     }
-    if (h == 0) slab[OFF_BIAS + col] = s_bias;
-    else        slab[OFF_B1 + col] = s_b1;
-    if (lane < kActions) slab[OFF_B2 + lane] = s_b2;
-    else if (lane == 63) slab[N_PARAMS] = s_loss;
   }
-  __syncthreads();
-  SWARM_STAMP(11);
-  // fixed-order sum of the block's TPB partial slabs -> one global slab
-  for (int p = threadIdx.x; p <= N_PARAMS; p += 128 * TPB) {
-    float acc = (&TW[0].T[0][0])[p];
+  __syncthreads();   // B3: dO / dH / das / dad
+  SWARM_STAMP(6);
+  // ---- products over B3's images: job 3: dW = dH^T X ; job 4: att sums ; job 5: dbias
+  //      online waves take jobs 3, 4 ; target waves job 5
+  for (int job = online ? 3 + wi : 5 + wi; job < (online ? 5 : 6); job += GPB) {
+    if (job == 3) {
+      f32x16 dW = {};
 #pragma unroll
-    for (int w = 1; w < TPB; ++w) acc = acc + (&TW[w].T[0][0])[p];
-    gslab[p] = acc;
+      for (int s = 0; s < 16; ++s) {
+        const int n = 2 * s + h;
+        dW = mfma32(TB.dH[n][col], col < 8 ? TB.X[n][col] : 0.0f, dW);
+      }
+      if (col < kFeat) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gslab[OFF_W + acc_row(r, h) * kFeat + col] = dW[r];
+      }
+    } else if (job == 4) {
+      float s_a = 0.0f;
+      if (h == 0) {
+        for (int n = 0; n < kTdRows; ++n) s_a = s_a + TB.das[n] * TB.H[n][col];
+        gslab[OFF_ATT_SRC + col] = s_a;
+      } else {
+        for (int n = 0; n < kTdRows; ++n) s_a = s_a + TB.dad[n] * TB.H[n][col];
+        gslab[OFF_ATT_DST + col] = s_a;
+      }
+    } else {
+      if (lane < kHidden) {
+        float s_bias = 0.0f;
+        for (int n = 0; n < kTdRows; ++n) s_bias = s_bias + TB.dO[n][lane];
+        gslab[OFF_BIAS + lane] = s_bias;
+      }
+    }
   }
-  SWARM_STAMP(12);
+  SWARM_STAMP(7);
 }
 
 // ---------------------------------------------------------------- slab reduction
@@ -506,22 +508,13 @@ __global__ void ctrl_advance_kernel(swarm_ctrl* C, int capacity) {
 using namespace swarm;
 
 namespace {
-int td_tiles(const swarm_config* cfg, int batch) {
-  const int E = kTile / cfg->n_agents;
-  return (batch + E - 1) / E;
-}
-// tiles per TD block (each tile = online wave + target wave); SWARM_TD_TPB=1|2|3 overrides
-int td_tpb_rt(int N) {
-  static int env = [] { const char* e = getenv("SWARM_TD_TPB"); return e ? atoi(e) : 0; }();
-  const int mx = N <= 16 ? 3 : 2;
-  int t = (env >= 1 && env <= 3) ? env : 1;   // measured: 1 tile per block is fastest (256 blocks)
-  return t < mx ? t : mx;
-}
+int td_slots(int N) { return N <= 8 ? 8 : (N <= 16 ? 16 : 32); }
+// one block per 32 node slots = 32 / NS sampled graphs
 int td_blocks(const swarm_config* cfg, int batch) {
-  const int w = td_tpb_rt(cfg->n_agents);
-  return (td_tiles(cfg, batch) + w - 1) / w;
+  const int gpb = kTdRows / td_slots(cfg->n_agents);
+  return (batch + gpb - 1) / gpb;
 }
-int td_max_blocks(const swarm_config* cfg, int batch) { return td_tiles(cfg, batch); }
+int td_max_blocks(const swarm_config* cfg, int batch) { return td_blocks(cfg, batch); }
 }  // namespace
 namespace {
 int check_td(const swarm_config* c, const swarm_adam_cfg* hp) {
@@ -555,12 +548,9 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.grad_scale = (float)(2.0 / ((double)hp->batch * (double)cfg->n_agents));
   const int nb = td_blocks(cfg, hp->batch);
   hipStream_t st = (hipStream_t)stream;
-  const int w = td_tpb_rt(a.N);
-#define SW_TD(NM, W) hipLaunchKernelGGL((td_kernel<NM, W>), dim3(nb), dim3(128 * W), 0, st, a)
-  if (a.N <= 8) { if (w == 1) SW_TD(8, 1); else if (w == 2) SW_TD(8, 2); else SW_TD(8, 3); }
-  else if (a.N <= 16) { if (w == 1) SW_TD(16, 1); else if (w == 2) SW_TD(16, 2); else SW_TD(16, 3); }
-  else { if (w == 1) SW_TD(32, 1); else SW_TD(32, 2); }
-#undef SW_TD
+  if (a.N <= 8) hipLaunchKernelGGL((td_kernel<8>), dim3(nb), dim3(128 * 4), 0, st, a);
+  else if (a.N <= 16) hipLaunchKernelGGL((td_kernel<16>), dim3(nb), dim3(128 * 2), 0, st, a);
+  else hipLaunchKernelGGL((td_kernel<32>), dim3(nb), dim3(128), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,389 @@
+// swarm_wpg.h — "wave per graph": one wave (64 lanes) owns ONE environment or
+// sampled graph of up to NS node slots (NS = 8, 16, 32).  Lane l works on node slot
+// s = l / G (G = 64 / NS lanes per slot) and owns the FPL = 32 / G contiguous hidden
+// features [f0, f0 + FPL), f0 = FPL * (l % G).
+//
+// Per-node vectors are therefore 4 (NS = 8) to 16 (NS = 32) registers per lane and
+// every dense per-node product is a k-ordered fmaf chain on the VALU; the full
+// 32-vector of a slot that a product needs is exchanged through a per-wave LDS row.
+// Reductions over a slot's feature groups are DPP butterflies (bitwise identical in
+// every lane of the slot); graph-wide exchange (scores, positions, Q rows) goes
+// through wave-private LDS with wave-scope syncs only — no workgroup barrier.
+//
+// GCN.forward: src/training/train_gcn_dqn.py:59-70 (GATConv -> tanh -> lin1 -> relu
+// -> lin2); GATConv math: PyG 2.5.3 (heads 1, add_self_loops False).
+#pragma once
+#include "swarm_common.h"
+#include "swarm_knn.h"
+
+namespace swarm {
+
+constexpr int kRow = 36;   // floats per LDS row of a 32-vector (32 + 4 pad, 16-B aligned)
+
+template <int NS>
+struct Wpg {
+  static_assert(NS == 8 || NS == 16 || NS == 32, "node slots per wave");
+  static constexpr int G = 64 / NS;          // lanes per node slot
+  static constexpr int FPL = kHidden / G;    // hidden features per lane
+  static constexpr int F4 = FPL / 4;         // float4 per lane-slice
+};
+
+// Copy the flat parameter vector into an LDS image once per block (every weight
+// read of the forward/backward then hits LDS).  All global loads are issued before
+// the first LDS write and none sits behind a branch (clamped index): one round trip.
+template <int NT>
+struct ParamStage {
+  static constexpr int NF4 = N_PARAMS / 4;            // 418 full float4 (floats 0..1671)
+  static constexpr int NJ = (NF4 + NT - 1) / NT;
+  float4 v[NJ];
+  float tail;
+  __device__ inline void load(const float* __restrict__ g, int tid) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = min(tid + j * NT, NF4 - 1);
+      v[j] = reinterpret_cast<const float4*>(g)[i];
+    }
+    tail = g[N_PARAMS - 1];
+  }
+  // into the padded LDS image (lds_index: lin1 / lin2 rows at a 36-float stride)
+  __device__ inline void store(float* __restrict__ lds, int tid) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = tid + j * NT;
+      if (i < NF4) *reinterpret_cast<float4*>(lds + lds_index(4 * i)) = v[j];
+    }
+    if (tid == 0) lds[lds_index(N_PARAMS - 1)] = tail;
+  }
+};
+static_assert(ParamStage<64>::NF4 * 4 + 1 == N_PARAMS && N_PARAMS_PAD == ParamStage<64>::NF4 * 4 + 4, "tail");
+
+// LDS traffic between lanes of ONE wave: LDS executes a wave's instructions in
+// order, so only compiler reordering has to be fenced (rocPRIM's wave_barrier).
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int CTRL>
+__device__ inline float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over the G contiguous lanes of a slot: quad_perm xor-1, xor-2, then
+// row_half_mirror (lane i <-> 7 - i inside 8 lanes); a + b == b + a, so every lane
+// of the slot ends with the bitwise same value.
+template <int G>
+__device__ inline float slot_sum(float x) {
+  x = x + dppf<0xB1>(x);
+  if constexpr (G >= 4) x = x + dppf<0x4E>(x);
+  if constexpr (G >= 8) x = x + dppf<0x141>(x);
+  static_assert(G == 2 || G == 4 || G == 8, "slot width");
+  return x;
+}
+
+template <int NS>
+struct WGeom {
+  int lane, s, q, f0;
+  int gid;      // env (acting) or batch index (TD) of this wave; 0 if the wave is idle
+  bool live;    // the wave has a graph
+  bool valid;   // live && s < N: this lane's slot is a real node
+};
+
+template <int NS>
+__device__ inline WGeom<NS> make_wgeom(int wave_gid, int count, int N) {
+  WGeom<NS> g;
+  g.lane = threadIdx.x & 63;
+  g.s = g.lane / Wpg<NS>::G;
+  g.q = g.lane % Wpg<NS>::G;
+  g.f0 = g.q * Wpg<NS>::FPL;
+  g.live = wave_gid < count;
+  g.gid = g.live ? wave_gid : 0;
+  g.valid = g.live && g.s < N;
+  return g;
+}
+
+// per-wave small LDS scratch
+template <int NS>
+struct WSmall {
+  float Q[NS][12];
+  float ssrc[NS], sdst[NS], px[NS], py[NS], aux[NS], aux2[NS];
+  uint32_t knn[NS];
+};
+
+// what one wave's forward reads and writes in LDS: NS rows of H, T (tanh out) and
+// R (relu out) — private scratch when acting, rows of the TD block's images in TD
+template <int NS>
+struct WView {
+  float (*H)[kRow];
+  float (*T)[kRow];
+  float (*R)[kRow];
+  WSmall<NS>* sm;
+};
+
+template <int NS>
+struct WScratch {
+  float H[NS][kRow], T[NS][kRow], R[NS][kRow];
+  WSmall<NS> sm;
+  __device__ WView<NS> view() { return WView<NS>{H, T, R, &sm}; }
+};
+
+// per-lane activations of the forward that the TD backward re-uses
+template <int NS>
+struct WFwd {
+  static constexpr int FPL = Wpg<NS>::FPL;
+  float x[8];          // node features (k < 7)
+  float h[FPL];        // conv1.lin output
+  float t[FPL];        // tanh(conv out)
+  float zr[(NS + 15) / 16][2][4];   // relu(lin1) in D layout (see mfma16 below)
+  float q[kActions];   // Q row of this lane's slot (every lane of the slot)
+  float sdst;          // destination score of this slot
+  float c[NS];         // coefficient of the in-edge u -> s (multiplicity x attention), 0 if none
+};
+
+template <int K>
+__device__ inline void lds_load(const float* __restrict__ p, float* out) {   // K floats, 16-B aligned
+#pragma unroll
+  for (int i = 0; i < K / 4; ++i) {
+    const float4 v = reinterpret_cast<const float4*>(p)[i];
+    out[4 * i] = v.x; out[4 * i + 1] = v.y; out[4 * i + 2] = v.z; out[4 * i + 3] = v.w;
+  }
+}
+template <int K>
+__device__ inline void lds_store(float* __restrict__ p, const float* in) {
+#pragma unroll
+  for (int i = 0; i < K / 4; ++i)
+    reinterpret_cast<float4*>(p)[i] = make_float4(in[4 * i], in[4 * i + 1], in[4 * i + 2], in[4 * i + 3]);
+}
+
+// ---- MFMA 16x16x4 f32 ("D layout").  D = A B with A [16 rows][4 k], B [4 k][16 cols]:
+// lane l supplies A[l & 15][kslot = l >> 4] and B[kslot = l >> 4][l & 15] and holds
+// D[4 (l >> 4) + r][l & 15], r = 0..3.  Here the columns are the graph's node slots
+// (column tile ct covers slots 16 ct .. 16 ct + 15) and the rows hidden features
+// (row tile t covers 16 t .. 16 t + 15): lane l holds features 16 t + 4 p + r of node
+// 16 ct + (l & 15), p = l >> 4.  A following product that sums over the feature index
+// takes those registers as its B operand directly: k-step (t, r) pairs k-slot p with
+// feature 16 t + 4 p + r.  Exact f32 (a k-ordered fmaf chain per instruction).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ inline f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+template <int NS> struct Dl { static constexpr int CT = (NS + 15) / 16; };
+
+// kNN row of slot s over the graph (simulator.py:17-19 -> CPU torch.topk set semantics)
+template <int NS>
+__device__ inline uint32_t knn_mask(const WGeom<NS>& g, int N, int k, const WSmall<NS>& sm) {
+  float d[NS];
+  const float xi = sm.px[g.s], yi = sm.py[g.s];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) d[j] = (j < N) ? norm2(sm.px[j] - xi, sm.py[j] - yi) : 0.0f;
+  return topk_smallest_mask<NS>(d, N, k);
+}
+
+// multiplicity m(u -> s) of every source slot u (target = this lane's slot)
+//   complete (train_gcn_dqn.py:101-108): u != v pairs plus one (0, 0) edge
+//   kNN (simulator.py:15-24): (i -> j) and (j -> i) for j in S_i, plus (0, 0)
+//   dense: caller-supplied [B][N][N] uint8
+template <int NS>
+__device__ inline void in_edges(const WGeom<NS>& g, int N, int graph, const WSmall<NS>& sm,
+                                const uint8_t* __restrict__ dense, int mult[NS]) {
+  const int s = g.valid ? g.s : 0;
+  const uint32_t ks = (graph == SWARM_GRAPH_KNN) ? sm.knn[s] : 0u;
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    int m = 0;
+    if (u < N && g.valid) {
+      if (graph == SWARM_GRAPH_COMPLETE) {
+        m = (u != s ? 1 : 0) + ((u == 0 && s == 0) ? 1 : 0);
+      } else if (graph == SWARM_GRAPH_KNN) {
+        m = (int)((sm.knn[u] >> s) & 1u) + (int)((ks >> u) & 1u) + ((u == 0 && s == 0) ? 1 : 0);
+      } else {
+        m = (int)dense[((size_t)g.gid * N + u) * N + s];
+      }
+    }
+    mult[u] = m;
+  }
+}
+
+// Full GCN.forward of the wave's graph.  F.x must hold this slot's features.  P is
+// the padded LDS weight image (lds_index).  Writes H/T/R rows and the per-slot
+// scalars of V; every lane ends with F.q, and F.zr holds relu(lin1) in D layout.
+template <int NS, int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
+__device__ inline void wpg_forward(const float* __restrict__ P, const WGeom<NS>& g, int N, int graph, int k,
+                                   int conv, const uint8_t* __restrict__ dense, const WView<NS>& V, WFwd<NS>& F) {
+#define WF_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
+  constexpr int G = Wpg<NS>::G, FPL = Wpg<NS>::FPL;
+  WSmall<NS>& sm = *V.sm;
+  const int s = g.s, f0 = g.f0;
+  // ---- conv1.lin (no bias): h = W x, K = 7
+  {
+    float w[FPL * kFeat];
+    lds_load<FPL * kFeat>(P + L_W + f0 * kFeat, w);
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) {
+      float a = w[i * kFeat] * F.x[0];
+#pragma unroll
+      for (int kk = 1; kk < kFeat; ++kk) a = fmaf(w[i * kFeat + kk], F.x[kk], a);
+      F.h[i] = a;
+    }
+  }
+  // ---- attention scores: (h * att).sum(-1)
+  float ssrc;
+  {
+    float as[FPL], ad[FPL];
+    lds_load<FPL>(P + L_ATT_SRC + f0, as);
+    lds_load<FPL>(P + L_ATT_DST + f0, ad);
+    float ps = 0.0f, pd = 0.0f;
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) { ps = ps + F.h[i] * as[i]; pd = pd + F.h[i] * ad[i]; }
+    ssrc = slot_sum<G>(ps);
+    F.sdst = slot_sum<G>(pd);
+  }
+  WF_STAMP(0);
+  lds_store<FPL>(&V.H[s][f0], F.h);
+  if (g.q == 0) { sm.ssrc[s] = ssrc; sm.sdst[s] = F.sdst; sm.px[s] = F.x[0]; sm.py[s] = F.x[1]; }
+  wave_lds_sync();
+  if (graph == SWARM_GRAPH_KNN) {
+    const uint32_t m = g.valid ? knn_mask<NS>(g, N, k, sm) : 0u;
+    if (g.q == 0) sm.knn[s] = m;
+    wave_lds_sync();
+  }
+  int mult[NS];
+  in_edges<NS>(g, N, graph, sm, dense, mult);
+  WF_STAMP(1);
+  // ---- attention softmax over in-edges (PyG softmax: exp(e - max) / (sum + 1e-16)),
+  //      duplicate edges counted by multiplicity; branch-free over the sources
+  if (conv == SWARM_CONV_GAT) {
+    float e[NS];
+    float emax = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const bool on = (u < N) && mult[u] > 0;
+      e[u] = leaky(sm.ssrc[u < N ? u : 0] + F.sdst);
+      emax = on ? fmaxf(emax, e[u]) : emax;
+    }
+    float den = 0.0f;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const bool on = (u < N) && mult[u] > 0;
+      e[u] = on ? __expf(e[u] - emax) : 0.0f;
+      den = den + (float)mult[u] * e[u];
+    }
+    den = den + 1e-16f;
+    const float inv = 1.0f / den;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) F.c[u] = (float)mult[u] * (e[u] * inv);
+  } else {
+    // GCNConv (a13, parity unpinned): self loops collapse to weight 1, symmetric deg^-1/2
+    float deg = 0.0f;
+#pragma unroll
+    for (int u = 0; u < NS; ++u)
+      if (u < N) deg = deg + (u == s ? 1.0f : (float)mult[u]);
+    const float dis = deg > 0.0f ? 1.0f / sqrtf(deg) : 0.0f;
+    if (g.q == 0) sm.aux[s] = g.valid ? dis : 0.0f;
+    wave_lds_sync();
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      F.c[u] = 0.0f;
+      if (u < N && g.valid) F.c[u] = (sm.aux[u] * (u == s ? 1.0f : (float)mult[u])) * dis;
+    }
+  }
+  WF_STAMP(2);
+  // ---- aggregate + bias + tanh
+  {
+    float out[FPL], b[FPL];
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) out[i] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      if (u < N) {   // uniform; c[u] == 0 for non-edges
+        float hv[FPL];
+        lds_load<FPL>(&V.H[u][f0], hv);
+#pragma unroll
+        for (int i = 0; i < FPL; ++i) out[i] = out[i] + F.c[u] * hv[i];
+      }
+    }
+    lds_load<FPL>(P + L_BIAS + f0, b);
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) F.t[i] = tanh_fast(out[i] + b[i]);
+  }
+  WF_STAMP(3);
+  lds_store<FPL>(&V.T[s][f0], F.t);
+  wave_lds_sync();
+  // ---- lin1 + relu on MFMA: Z^T[feature][node] = W1 T^T, K = 32 in 8 k-steps of 4
+  //      (k-step s pairs k-slot p with k = 4 s + p)
+  const int c = g.lane & 15, p = g.lane >> 4;
+  {
+    float a1[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) a1[t][ks] = P[L_W1 + (16 * t + c) * kWRow + 4 * ks + p];
+    const float4 b1a = *reinterpret_cast<const float4*>(P + L_B1 + 4 * p);
+    const float4 b1b = *reinterpret_cast<const float4*>(P + L_B1 + 16 + 4 * p);
+    const float b1v[2][4] = {{b1a.x, b1a.y, b1a.z, b1a.w}, {b1b.x, b1b.y, b1b.z, b1b.w}};
+#pragma unroll
+    for (int ct = 0; ct < Dl<NS>::CT; ++ct) {
+      const int n = min(16 * ct + c, NS - 1);   // columns past NS: clamped reads, results unused
+      f32x4 z0 = {0.f, 0.f, 0.f, 0.f}, z1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const float b = V.T[n][4 * ks + p];
+        z0 = mfma16(a1[0][ks], b, z0);
+        z1 = mfma16(a1[1][ks], b, z1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float u0 = z0[r] + b1v[0][r], u1 = z1[r] + b1v[1][r];
+        F.zr[ct][0][r] = u0 > 0.0f ? u0 : 0.0f;
+        F.zr[ct][1][r] = u1 > 0.0f ? u1 : 0.0f;
+      }
+      if (16 * ct + c < NS) {   // natural-order R row (TD products)
+        *reinterpret_cast<float4*>(&V.R[16 * ct + c][4 * p]) =
+            make_float4(F.zr[ct][0][0], F.zr[ct][0][1], F.zr[ct][0][2], F.zr[ct][0][3]);
+        *reinterpret_cast<float4*>(&V.R[16 * ct + c][16 + 4 * p]) =
+            make_float4(F.zr[ct][1][0], F.zr[ct][1][1], F.zr[ct][1][2], F.zr[ct][1][3]);
+      }
+    }
+  }
+  WF_STAMP(4);
+  // ---- lin2 on MFMA: Q^T[action][node] = W2 R^T; the relu registers are the B operand
+  //      (k-step (t, r) -> k = 16 t + 4 p + r); A rows >= 9 are zero
+  {
+    float a2[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c < kActions) w = *reinterpret_cast<const float4*>(P + L_W2 + c * kWRow + 16 * t + 4 * p);
+      a2[t][0] = w.x; a2[t][1] = w.y; a2[t][2] = w.z; a2[t][3] = w.w;
+    }
+#pragma unroll
+    for (int ct = 0; ct < Dl<NS>::CT; ++ct) {
+      f32x4 qa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qa = mfma16(a2[t][r], F.zr[ct][t][r], qa);
+      const int n = 16 * ct + c;
+      if (n < NS && p < 3) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = 4 * p + r;
+          if (a < kActions) sm.Q[n][a] = qa[r] + P[L_B2 + a];
+        }
+      }
+    }
+  }
+  wave_lds_sync();
+  {
+    const float4 q0 = *reinterpret_cast<const float4*>(&sm.Q[s][0]);
+    const float4 q1 = *reinterpret_cast<const float4*>(&sm.Q[s][4]);
+    F.q[0] = q0.x; F.q[1] = q0.y; F.q[2] = q0.z; F.q[3] = q0.w;
+    F.q[4] = q1.x; F.q[5] = q1.y; F.q[6] = q1.z; F.q[7] = q1.w;
+    F.q[8] = sm.Q[s][8];
+  }
+  WF_STAMP(5);
+#undef WF_STAMP
+}
+
+}  // namespace swarm

@@ -4,7 +4,7 @@ In the reference these are VMAS ``BaseScenario`` subclasses whose
 ``reset_world_at`` / ``reward`` / ``observation`` VMAS calls on every step
 (src/scenarios/go_to_position_scenario.py, src/scenarios/obstacle_avoidance_scenario.py).
 Here the arithmetic of those methods lives in the HIP kernels
-(``csrc/swarm_tile.h`` agent_step / oa_reward, ``csrc/swarm_act.hip`` reset);
+(``csrc/swarm_env.h`` agent_step / oa_reward, ``csrc/swarm_act.hip`` reset);
 the classes carry the configuration and expose the metric helpers the
 reference's callers use (``average_distance_to_goal``, ``obstacles_hits``,
 ``average_distance_to_obstacles``; simulator.py:62-87), computed from the

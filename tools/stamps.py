@@ -15,19 +15,19 @@ import torch  # noqa: E402
 import swarm_amd  # noqa: E402
 from swarm_amd import _lib  # noqa: E402
 
-ACT = {0: "entry", 1: "prologue(state+params->LDS)", 2: "lin0+scores+H->LDS", 3: "barrier+graph_mult",
-       4: "softmax+aggregate", 5: "tanh", 6: "lin1(MFMA)+relu", 7: "lin2(VALU)", 8: "eps-greedy(philox)",
-       9: "agent_step(physics)", 10: "reward/metrics(LDS)", 11: "stores+barrier", 12: "end"}
-TD = {0: "entry", 1: "params loads+ctrl+skip", 2: "sample_index(feistel)", 3: "replay loads+LDS stage+barrier",
-      16: "fwd lin0+scores", 17: "barrier+graph_mult", 18: "softmax+aggregate", 19: "tanh", 20: "lin1",
-      21: "lin2", 4: "(y)", 5: "barrier (y ready)", 6: "MLP backward (W2,relu,W1^T MFMA,tanh')",
-      7: "image writes+barrier", 8: "GAT attn bwd | dW1,dW2,sums  +barrier", 9: "dh messages+barrier",
-      10: "dW + datt", 11: "partial slab write+barrier", 12: "block slab sum+store"}
+FWD = {0: "fwd lin0 + scores", 1: "fwd H/scalars -> LDS, in-edges", 2: "fwd softmax",
+       3: "fwd aggregate + tanh", 4: "fwd T exchange + lin1", 5: "fwd R exchange + lin2 + Q exchange"}
+ACT = {0: "entry", 1: "prologue (state + Adam/params -> LDS + barrier)", **{8 + k: v for k, v in FWD.items()},
+       2: "(end of forward)",
+       3: "eps-greedy + physics", 4: "reward/metrics + stores"}
+TD = {0: "entry", 1: "params loads + ctrl + skip + sample index", 2: "replay loads + LDS stage + barrier",
+      **{16 + k: v for k, v in FWD.items()}, 3: "(y)", 4: "barrier (y ready)", 5: "dQ/dZ images + barrier",
+      6: "dT/dO/GAT bwd/dh | dW1,dW2,b1 products + barrier", 7: "dW / att / bias products"}
 
 
 def report(buf, names, nwaves):
     a = buf.reshape(-1, 32)[:nwaves].astype(np.int64)
-    order = sorted(names, key=lambda k: (k if k < 16 else 3.5 + (k - 16) * 0.01))
+    order = sorted(names, key=lambda k: (k if k < 8 else (1.5 + (k - 8) * 0.01 if k < 16 else 2.5 + (k - 16) * 0.01)))
     order = [k for k in order if (a[:, k] > 0).all()]
     tot = np.median(a[:, order[-1]] - a[:, order[0]])
     print(f"  total median {tot:.0f} cycles")
@@ -54,17 +54,17 @@ def main():
     for _ in range(3):
         eng.train_tick()
     torch.cuda.synchronize()
-    tiles = (B + (32 // N) - 1) // (32 // N)
-    ab = (tiles + 3) // 4
-    print(f"act_kernel ({ab} blocks x 4 waves):")
+    ab = (B + 3) // 4
+    print(f"act_kernel ({ab} blocks x 4 waves, one env per wave):")
     report(sa.cpu().numpy()[: ab * 16 * 32].reshape(ab, 16, 32)[:, :4].reshape(-1), ACT, ab * 4)
-    tpb = int(os.environ.get("SWARM_TD_TPB", 1))
-    blocks = (tiles + tpb - 1) // tpb
+    ns = 8 if N <= 8 else (16 if N <= 16 else 32)
+    gpb = 32 // ns
+    blocks = (B + gpb - 1) // gpb
     td = st.cpu().numpy()[: blocks * 16 * 32].reshape(blocks, 16, 32)
-    print(f"td_kernel ({blocks} blocks x {tpb} tiles), online waves:")
-    report(td[:, :tpb].reshape(-1), TD, blocks * tpb)
+    print(f"td_kernel ({blocks} blocks x {gpb} graphs), online waves:")
+    report(td[:, :gpb].reshape(-1), TD, blocks * gpb)
     print("td_kernel target waves:")
-    report(td[:, tpb:2 * tpb].reshape(-1), TD, blocks * tpb)
+    report(td[:, gpb:2 * gpb].reshape(-1), TD, blocks * gpb)
 
 
 if __name__ == "__main__":
