@@ -53,7 +53,8 @@ class SwarmLearner(ctypes.Structure):
 
 # swarm_ctrl is 16 x 4-byte words on the device; field -> word index
 CTRL_WORDS = 16
-CTRL = dict(tick=0, write_slot=1, filled_slots=2, adam_step=3, eps=4, loss=5, grad_norm=6, trained=7, episode=8)
+CTRL = dict(tick=0, write_slot=1, filled_slots=2, adam_step=3, eps=4, loss=5, grad_norm=6, trained=7, episode=8,
+            adam_step_size=14, adam_inv_bc2=15)
 
 _PROTOS = {
     "swarm_abi_version": (c_int32, []),
@@ -82,6 +83,7 @@ _PROTOS = {
     "swarm_grad_reduce": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p, c_void_p, c_void_p]),
     "swarm_adam_step": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "swarm_ctrl_init": (c_int32, [POINTER(SwarmAdamCfg), c_float, c_void_p, c_void_p]),
     "swarm_ctrl_advance": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmReplay), c_void_p, c_void_p]),
     "swarm_host_topk_set": (c_int32, [POINTER(c_float), c_int32, c_int32, POINTER(ctypes.c_uint8)]),
 }

@@ -72,11 +72,12 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
     R.load(A.lr.grad, A.lr.w_cur, A.lr.m_cur, A.lr.v_cur, tid);
     const uint32_t pending = A.ctrl->trained;
     const uint32_t tnow = A.ctrl->tick;
-    const double b1pow = ctrl_get_double(A.ctrl, CTRL_B1POW) * (double)A.hp.beta1;
-    const double b2pow = ctrl_get_double(A.ctrl, CTRL_B2POW) * (double)A.hp.beta2;
+    const float step_size = A.ctrl->adam_step_size, inv_bc2 = A.ctrl->adam_inv_bc2;
     float gn = 0.0f;
-    if (pending) gn = adam_apply(R, A.hp, b1pow, b2pow, tid, red);
+    SWARM_STAMP(20);
+    if (pending) gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, tid, red);
     store_w_lds(Pw, R, tid);
+    SWARM_STAMP(24);
     if (blockIdx.x == 0) {
       store4(A.lr.w_nxt, R.w, R.wt, tid);
       store4(A.lr.m_nxt, R.m, R.mt, tid);
@@ -146,9 +147,37 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       }
     }
 
-    // ---- env.step (VMAS World.step + scenario reward)
-    const StepOut o = agent_step<NS>(A.scenario, N, agent, px, py, vx, vy, action,
-                                     [&](int u, float& ux, float& uy) { ux = sm.px[u]; uy = sm.py[u]; });
+    // ---- env.step (VMAS World.step + scenario reward).  The G lanes of a slot split the
+    //      partner pairs (lane q: partners q, q + G, ...; the contact branch runs once per
+    //      lane instead of once per partner), then every lane sums the forces in VMAS
+    //      order: 0 + u, obstacle pair, agent pairs in ascending partner index (SURVEY
+    //      a1-a3); -f(p_u - p_v) == f(p_v - p_u) bit for bit.  Scratch: the H/T/R rows,
+    //      free after the forward.
+    float* fb = &SW[w].H[0][0];
+    static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
+#pragma unroll
+    for (int j = 0; j < NS / Wpg<NS>::G; ++j) {
+      const int u = g.q + j * Wpg<NS>::G;
+      float gx = 0.0f, gy = 0.0f;
+      if (u < N) pair_force(px - sm.px[u], py - sm.py[u], gx, gy);   // u == agent: exactly 0
+      *reinterpret_cast<float2*>(fb + 2 * (g.s * NS + u)) = make_float2(gx, gy);
+    }
+    float fx = 0.0f + action_level(action / 3);
+    float fy = 0.0f + action_level(action % 3);
+    if (A.scenario == SWARM_OBSTACLE_AVOIDANCE) {
+      float gx, gy;
+      pair_force(px - kObstX, py - kObstY, gx, gy);
+      fx = fx + gx; fy = fy + gy;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      if (u < N) {
+        const float2 f = *reinterpret_cast<const float2*>(fb + 2 * (g.s * NS + u));
+        fx = fx + f.x; fy = fy + f.y;
+      }
+    }
+    const StepOut o = integrate(px, py, vx, vy, fx, fy);
     if (it == 0) SWARM_STAMP(3);
     if (g.q == 0) { sm.aux[g.s] = o.dgoal; sm.aux2[g.s] = (o.dobs <= 0.2f) ? 1.0f : 0.0f; }
     wave_lds_sync();

@@ -38,6 +38,17 @@ __device__ inline void ctrl_set_double(swarm_ctrl* c, int word, double v) {
 constexpr int CTRL_B1POW = 0;   // beta_pow[0..1] = beta1^adam_step
 constexpr int CTRL_B2POW = 2;   // beta_pow[2..3] = beta2^adam_step
 
+// Adam scalars of the step after the one ctrl's beta powers describe (torch single_tensor:
+// step_size = lr / bias_correction1, bias_correction2_sqrt = sqrt(bias_correction2), both
+// in double), stored in ctrl as floats by whoever advances the powers, so the optimizer
+// step itself carries no double-precision work.  One function for every path.
+__device__ inline void ctrl_store_next_scalars(swarm_ctrl* c, const swarm_adam_cfg& hp) {
+  const double b1n = ctrl_get_double(c, CTRL_B1POW) * (double)hp.beta1;
+  const double b2n = ctrl_get_double(c, CTRL_B2POW) * (double)hp.beta2;
+  c->adam_step_size = (float)((double)hp.lr / (1.0 - b1n));
+  c->adam_inv_bc2 = 1.0f / (float)sqrt(1.0 - b2n);
+}
+
 struct AdamRegs {
   float4 g[kAdamNJ], w[kAdamNJ], m[kAdamNJ], v[kAdamNJ];
   float gt, wt, mt, vt;    // tail element N_PARAMS - 1
@@ -57,28 +68,43 @@ struct AdamRegs {
   }
 };
 
+template <int CTRL>
+__device__ inline float adam_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// wave-wide sum, fixed order: DPP butterflies inside each 16-lane row (quad_perm xor-1,
+// xor-2, row_half_mirror, row_mirror), then the four row sums in row order
 __device__ inline float wave_sum(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);
-  return x;
+  x = x + adam_dpp<0xB1>(x);
+  x = x + adam_dpp<0x4E>(x);
+  x = x + adam_dpp<0x141>(x);
+  x = x + adam_dpp<0x140>(x);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+  return ((r0 + r1) + r2) + r3;
 }
 
-// torch divides twice per element; here both divisions are reciprocal multiplies
-// (<= 1-2 ulp per step, inside the 2e-6 parameter tolerance of the parity tests).
+// torch divides twice per element; here both divisions are reciprocal multiplies and
+// the square root is v_sqrt_f32 (<= 1-2 ulp per step, inside the 2e-6 parameter
+// tolerance of the parity tests).
 __device__ inline void adam_elem(float g, float& w, float& m, float& v, float one_m_b1, float beta2,
                                  float one_m_b2, float inv_bc2_sqrt, float eps, float step_size) {
   m = m + one_m_b1 * (g - m);
   v = v * beta2;
   v = v + one_m_b2 * g * g;
-  const float denom = sqrtf(v) * inv_bc2_sqrt + eps;
+  const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2_sqrt + eps;
   w = w + (-step_size) * (m * __builtin_amdgcn_rcpf(denom));
 }
 
 // One optimizer step in registers by the whole workgroup (kAdamNT threads; contains
-// __syncthreads).  b1pow/b2pow = beta^step for this (1-based) step.  Returns the
+// __syncthreads).  step_size / inv_bc2_sqrt: ctrl's scalars of this step.  Returns the
 // pre-clip global norm.  red: LDS scratch of >= 8 * (kAdamNT/64) + 8 floats.
-__device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, double b1pow, double b2pow, int tid,
-                                   float* red) {
+template <int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
+__device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float step_size, float inv_bc2_sqrt,
+                                   int tid, float* red) {
+#define AD_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
   const float inv_w = 1.0f / (float)hp.world_size;
   float ss[8];
 #pragma unroll
@@ -96,6 +122,7 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, double
   }
   if (hp.world_size > 1) R.gt = R.gt * inv_w;
   if (tid == 0) ss[7] = ss[7] + R.gt * R.gt;
+  AD_STAMP(0);
   constexpr int NW = kAdamNT / 64;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -113,12 +140,10 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, double
     nn = nn + nk * nk;
   }
   const float total_norm = sqrtf(nn);
+  AD_STAMP(1);
   const float coef = hp.max_norm / (total_norm + 1e-6f);
   const float clamped = coef < 1.0f ? coef : 1.0f;
-  const double bc1 = 1.0 - b1pow;
-  const double bc2 = 1.0 - b2pow;
-  const float step_size = (float)((double)hp.lr / bc1);
-  const float bc2_sqrt = 1.0f / (float)sqrt(bc2);   // reciprocal of sqrt(bias_correction2)
+  const float bc2_sqrt = inv_bc2_sqrt;   // reciprocal of sqrt(bias_correction2)
   const float one_m_b1 = (float)(1.0 - (double)hp.beta1);
   const float one_m_b2 = (float)(1.0 - (double)hp.beta2);
 #pragma unroll
@@ -131,6 +156,8 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, double
     R.w[j] = w; R.m[j] = m; R.v[j] = v;
   }
   adam_elem(R.gt * clamped, R.wt, R.mt, R.vt, one_m_b1, hp.beta2, one_m_b2, bc2_sqrt, hp.eps, step_size);
+  AD_STAMP(2);
+#undef AD_STAMP
   return total_norm;
 }
 

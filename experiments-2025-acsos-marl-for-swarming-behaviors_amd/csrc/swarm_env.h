@@ -13,30 +13,9 @@ struct StepOut {
   float dobs;             // World.get_distance(agent, obstacle) (OA)
 };
 
-// VMAS World.step for agent `agent` of an env whose pre-step positions are read
-// through pos(u).  Force order: 0 + u, obstacle pair, agent pairs in ascending
-// partner index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
-template <int NMAX, typename PosFn>
-__device__ inline StepOut agent_step(int scenario, int N, int agent, float px, float py, float vx, float vy,
-                                     int action, PosFn pos) {
-  float ux[NMAX], uy[NMAX];
-#pragma unroll
-  for (int u = 0; u < NMAX; ++u) pos(u < N ? u : 0, ux[u], uy[u]);   // all reads issued first
-  float fx = 0.0f + action_level(action / 3);
-  float fy = 0.0f + action_level(action % 3);
-  if (scenario == SWARM_OBSTACLE_AVOIDANCE) {
-    float gx, gy;
-    pair_force(px - kObstX, py - kObstY, gx, gy);
-    fx = fx + gx; fy = fy + gy;
-  }
-#pragma unroll
-  for (int u = 0; u < NMAX; ++u) {
-    if (u < N) {
-      float gx, gy;
-      pair_force(px - ux[u], py - uy[u], gx, gy);   // u == agent: dist 0 < 1e-6 -> exactly 0
-      fx = fx + gx; fy = fy + gy;
-    }
-  }
+// Drag + Euler and the scenario distances of one agent after its force sum (VMAS
+// World._integrate_state, dt 0.1, drag 0.25, mass 1).
+__device__ inline StepOut integrate(float px, float py, float vx, float vy, float fx, float fy) {
   StepOut o;
   o.vx = vx * kDragKeep;
   o.vy = vy * kDragKeep;

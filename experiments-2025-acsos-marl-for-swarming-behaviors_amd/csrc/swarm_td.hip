@@ -361,7 +361,7 @@ struct ReduceArgs {
   swarm_learner lr;
   swarm_ctrl* ctrl;
   int capacity, B, N, batch;
-  float beta1, beta2;
+  swarm_adam_cfg hp;
   int32_t* sample_next;   // fused tick: replay indices of the NEXT tick's TD batch
   uint32_t k0, k1;        // sampling key (seed ^ rank salt)
 };
@@ -423,8 +423,9 @@ __global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs
       const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
       if (C->trained) {                                   // applied by this tick's act kernel
         C->adam_step = C->adam_step + 1;
-        ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * (double)A.beta1);
-        ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * (double)A.beta2);
+        ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * (double)A.hp.beta1);
+        ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * (double)A.hp.beta2);
+        ctrl_store_next_scalars(C, A.hp);
       }
       C->trained = trained;
       C->loss = trained ? tot / (float)((size_t)A.batch * A.N) : 0.0f;
@@ -461,8 +462,7 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
   const uint32_t tick = C->tick;
   const uint32_t step = C->adam_step + 1;
-  const double b1pow = ctrl_get_double(C, CTRL_B1POW) * (double)A.hp.beta1;
-  const double b2pow = ctrl_get_double(C, CTRL_B2POW) * (double)A.hp.beta2;
+  const float step_size = C->adam_step_size, inv_bc2 = C->adam_inv_bc2;
   const bool train = A.flush ? (C->trained != 0u) : (valid_slots * (uint32_t)A.B >= (uint32_t)A.hp.batch);
   // target sync: unfused = after the TD step of tick `tick` ((tick+1) % every); flush = the
   // fused tick already advanced ctrl, so the pending update belongs to tick - 1
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
   __syncthreads();   // every thread has read ctrl before thread 0 rewrites it
   float gn = 0.0f;
   if (train) {
-    gn = adam_apply(R, A.hp, b1pow, b2pow, tid, red);
+    gn = adam_apply(R, A.hp, step_size, inv_bc2, tid, red);
     store4(A.params, R.w, R.wt, tid);
     store4(A.m, R.m, R.mt, tid);
     store4(A.v, R.v, R.vt, tid);
@@ -480,8 +480,9 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
     if (train) {
       C->adam_step = step;
       C->grad_norm = gn;
-      ctrl_set_double(C, CTRL_B1POW, b1pow);
-      ctrl_set_double(C, CTRL_B2POW, b2pow);
+      ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * (double)A.hp.beta1);
+      ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * (double)A.hp.beta2);
+      ctrl_store_next_scalars(C, A.hp);
     }
     if (A.flush) {
       C->trained = 0u;
@@ -494,6 +495,15 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
       C->filled_slots = valid_slots;
     }
   }
+}
+
+__global__ void ctrl_init_kernel(swarm_adam_cfg hp, float eps, swarm_ctrl* C) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(C);
+  for (int i = 0; i < (int)(sizeof(swarm_ctrl) / 4); ++i) w[i] = 0u;
+  C->eps = eps;
+  ctrl_set_double(C, CTRL_B1POW, 1.0);
+  ctrl_set_double(C, CTRL_B2POW, 1.0);
+  ctrl_store_next_scalars(C, hp);
 }
 
 __global__ void ctrl_advance_kernel(swarm_ctrl* C, int capacity) {
@@ -575,7 +585,7 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = lr->grad;
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
-  a.beta1 = hp->beta1; a.beta2 = hp->beta2;
+  a.hp = *hp;
   a.sample_next = sample_next;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
@@ -626,6 +636,12 @@ int swarm_adam_flush(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   if (int e = check_td(cfg, hp)) return e;
   if (!lr || !ctrl) return SWARM_E_BADARG;
   return launch_adam(cfg, hp, lr->w_cur, lr->target, lr->m_cur, lr->v_cur, lr->grad, 1, ctrl, 1, stream);
+}
+
+int swarm_ctrl_init(const swarm_adam_cfg* hp, float eps, swarm_ctrl* ctrl, void* stream) {
+  if (!hp || !ctrl) return SWARM_E_BADARG;
+  hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, *hp, eps, ctrl);
+  return (int)hipGetLastError();
 }
 
 int swarm_ctrl_advance(const swarm_config* cfg, const swarm_replay* replay, swarm_ctrl* ctrl, void* stream) {

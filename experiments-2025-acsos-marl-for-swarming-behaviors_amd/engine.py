@@ -122,8 +122,8 @@ class SwarmEngine:
         self.params.copy_(p0)
         self.target.copy_(p0)
         self.ctrl = torch.zeros(_lib.CTRL_WORDS, dtype=torch.int32, device=dev)
-        self.ctrl.view(torch.float64)[5:7] = 1.0     # words 10-13: beta1^0, beta2^0
-        self.set_eps(eps)
+        check(self.lib.swarm_ctrl_init(ctypes_ref(self.hp), float(eps), ptr(self.ctrl), stream_ptr()),
+              "swarm_ctrl_init")
         self.episode = 0
         cap = max(1, -(-replay_capacity // n_envs)) if learn else 1
         self.capacity = cap

@@ -63,10 +63,12 @@ typedef struct swarm_ctrl {
                              swarm_train_act_step or by swarm_adam_flush); 0 after swarm_adam_step */
   uint32_t episode;       /* episode counter (reset RNG key)                                */
   uint32_t pad0;
-  uint32_t beta_pow[4];   /* beta1^adam_step, beta2^adam_step as two little-endian doubles;
-                             initialise both to 1.0 (words 10-13)                          */
-  uint32_t pad[2];
+  uint32_t beta_pow[4];   /* beta1^adam_step, beta2^adam_step as two little-endian doubles
+                             (words 10-13)                                                  */
+  float adam_step_size;   /* Adam scalars of optimizer step adam_step + 1, kept current by the */
+  float adam_inv_bc2;     /* library: lr / (1 - beta1^(s+1)) and 1 / sqrt(1 - beta2^(s+1))     */
 } swarm_ctrl;
+/* A fresh control block comes from swarm_ctrl_init (all counters 0, beta powers 1). */
 
 /* Replay ring (GraphReplayBuffer, train_gcn_dqn.py:25-48), SoA, per rank:
  * slot t holds the B transitions pushed at one tick. Graph id g = slot*B + env. */
@@ -213,6 +215,9 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
 int swarm_adam_step(const swarm_config* cfg, const swarm_adam_cfg* hp, float* params,
                     float* target, float* adam_m, float* adam_v, const float* grad,
                     int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
+
+/* Initialise a control block: counters 0, eps, beta^0 = 1 and the Adam scalars of step 1. */
+int swarm_ctrl_init(const swarm_adam_cfg* hp, float eps, swarm_ctrl* ctrl, void* stream);
 
 /* Advance ctrl after an acting-only tick (no optimizer). */
 int swarm_ctrl_advance(const swarm_config* cfg, const swarm_replay* replay, swarm_ctrl* ctrl, void* stream);

@@ -17,7 +17,9 @@ from swarm_amd import _lib  # noqa: E402
 
 FWD = {0: "fwd lin0 + scores", 1: "fwd H/scalars -> LDS, in-edges", 2: "fwd softmax",
        3: "fwd aggregate + tanh", 4: "fwd T exchange + lin1", 5: "fwd R exchange + lin2 + Q exchange"}
-ACT = {0: "entry", 1: "prologue (state + Adam/params -> LDS + barrier)", **{8 + k: v for k, v in FWD.items()},
+ACT = {0: "entry", 20: "pro: loads issued + ctrl", 21: "pro: norm partials (data arrival)",
+       22: "pro: norm reduction (barrier)", 23: "pro: Adam elements", 24: "pro: w -> LDS",
+       1: "pro: barrier", **{8 + k: v for k, v in FWD.items()},
        2: "(end of forward)",
        3: "eps-greedy + physics", 4: "reward/metrics + stores"}
 TD = {0: "entry", 1: "params loads + ctrl + skip + sample index", 2: "replay loads + LDS stage + barrier",
@@ -27,7 +29,7 @@ TD = {0: "entry", 1: "params loads + ctrl + skip + sample index", 2: "replay loa
 
 def report(buf, names, nwaves):
     a = buf.reshape(-1, 32)[:nwaves].astype(np.int64)
-    order = sorted(names, key=lambda k: (k if k < 8 else (1.5 + (k - 8) * 0.01 if k < 16 else 2.5 + (k - 16) * 0.01)))
+    order = sorted(names, key=lambda k: (k if k < 8 else (1.5 + (k - 8) * 0.01 if k < 16 else (2.5 + (k - 16) * 0.01 if k < 20 else 0.5 + (k - 20) * 0.01))))
     order = [k for k in order if (a[:, k] > 0).all()]
     tot = np.median(a[:, order[-1]] - a[:, order[0]])
     print(f"  total median {tot:.0f} cycles")
