@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["swarm_act.hip", "swarm_td.hip"]
-HEADERS = ["swarm_common.h", "swarm_knn.h", "swarm_wpg.h", "swarm_env.h", "swarm_adam.h"]
+HEADERS = ["swarm_common.h", "swarm_knn.h", "swarm_wpg.h", "swarm_dl.h", "swarm_env.h", "swarm_adam.h"]
 OUT = os.path.join(HERE, "libswarm_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",

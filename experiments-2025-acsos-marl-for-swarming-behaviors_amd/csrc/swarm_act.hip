@@ -9,7 +9,7 @@
 
 #include "swarm_adam.h"
 #include "swarm_env.h"
-#include "swarm_wpg.h"
+#include "swarm_dl.h"
 
 namespace swarm {
 
@@ -37,32 +37,41 @@ struct ActArgs {
 
 constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
 
-// One wave per environment (swarm_wpg.h).  Block-wide work is only the weight image
-// (LDS) — staged from global memory or produced by the fused Adam prologue.
+// One wave per environment in the D layout (swarm_dl.h): lane (c, p) serves agent
+// n = 16 ct + c with row group p.  Block-wide work is only the weight image (LDS),
+// staged from global memory or produced by the fused Adam prologue.
 template <int NS, int MODE>
 __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
+  constexpr int CT = DGeom<NS>::CT;
   __shared__ WScratch<NS> SW[kActWPB];
   __shared__ __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
   __shared__ float red[8 * kActWPB + 8];
   SWARM_STAMP(0);
   const int w = threadIdx.x >> 6;
   const int N = A.N;
-  const WGeom<NS> g = make_wgeom<NS>(blockIdx.x * kActWPB + w, A.B, N);
+  const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * kActWPB + w, A.B);
   const WView<NS> V = SW[w].view();
   WSmall<NS>& sm = SW[w].sm;
-  const int agent = g.valid ? g.s : 0;                 // idle slots alias agent 0: in-bounds reads, no writes
-  const size_t node = (size_t)g.gid * N + agent;
-  const bool writer = g.valid && g.q == 0;             // one lane per node slot stores
+  const int c = d.c, p = d.p;
 
   // prologue: every independent global load in flight at once
-  WFwd<NS> F;
-  float px = 0.f, py = 0.f, vx = 0.f, vy = 0.f;
-  if (MODE == MODE_Q) {
+  DFwd<NS> F;
+  float px[CT], py[CT], vx[CT], vy[CT];
+  bool valid[CT];
+  size_t node[CT];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) F.x[k] = (k < kFeat && g.valid) ? A.x[node * kFeat + k] : 0.0f;
-  } else {
-    const float4 st = *reinterpret_cast<const float4*>(A.state + node * 4);
-    if (g.valid) { px = st.x; py = st.y; vx = st.z; vy = st.w; }
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = 16 * ct + c;
+    valid[ct] = d.live && n < N;
+    node[ct] = (size_t)d.gid * N + min(n, N - 1);   // idle lanes alias an in-bounds node, never store
+    px[ct] = py[ct] = vx[ct] = vy[ct] = 0.0f;
+    if (MODE == MODE_Q) {
+      F.x[ct][0] = valid[ct] ? A.x[node[ct] * kFeat + p] : 0.0f;
+      F.x[ct][1] = (valid[ct] && 4 + p < kFeat) ? A.x[node[ct] * kFeat + 4 + p] : 0.0f;
+    } else {
+      const float4 st = *reinterpret_cast<const float4*>(A.state + node[ct] * 4);
+      if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
+    }
   }
   if (MODE == MODE_TICK && A.learn) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
@@ -103,83 +112,95 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
     slot = A.ctrl->write_slot;
   }
   const int n_ticks = (MODE == MODE_ROLLOUT) ? A.n_ticks : 1;
-  float rew_sum = 0.0f, hits_sum = 0.0f;
+  float rew_sum[CT], hits_sum = 0.0f;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) rew_sum[ct] = 0.0f;
+  float* fb = &SW[w].H[0][0];   // pair-force scratch [NS][NS][2] (H/T/R rows are free after the forward)
+  static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
 
   for (int it = 0; it < n_ticks; ++it) {
     if (MODE != MODE_Q) {
-      F.x[0] = px; F.x[1] = py; F.x[2] = vx; F.x[3] = vy;
-      F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)agent; F.x[7] = 0.0f;
-      if (!g.valid) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
+      for (int ct = 0; ct < CT; ++ct) {
+        node_x(px[ct], py[ct], vx[ct], vy[ct], 16 * ct + c, p, F.x[ct]);
+        if (!valid[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
       }
     }
     if (MODE != MODE_STEP) {
-      wpg_forward<NS, 8>(P, g, N, A.graph, A.k, A.conv, A.dense, V, F);
+      dl_forward<NS, 8>(P, d, N, A.graph, A.k, A.conv, A.dense, V, false, F);
     } else {
-      if (g.q == 0) { sm.px[g.s] = px; sm.py[g.s] = py; }
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        if (16 * ct + c < NS && p == 0) { sm.px[16 * ct + c] = px[ct]; sm.py[16 * ct + c] = py[ct]; }
       wave_lds_sync();
     }
     if (it == 0) SWARM_STAMP(2);
 
-    if (MODE == MODE_Q) {
-      if (g.valid) {   // lanes of the slot store the Q row together (from LDS: no dynamic register index)
+    if (MODE == MODE_Q) {   // the node's row groups store its Q row (from LDS: no lane-indexed registers)
 #pragma unroll
-        for (int j = 0; j < (kActions + Wpg<NS>::G - 1) / Wpg<NS>::G; ++j) {
-          const int a = g.q + j * Wpg<NS>::G;
-          if (a < kActions) A.out.q[node * kActions + a] = sm.Q[g.s][a];
-        }
-      }
+      for (int ct = 0; ct < CT; ++ct)
+        if (valid[ct])
+          for (int a = p; a < kActions; a += 4) A.out.q[node[ct] * kActions + a] = sm.Q[16 * ct + c][a];
       return;
     }
 
     // ---- eps-greedy (train_gcn_dqn.py:164-167), one Philox coin per env and tick
     const uint32_t tk = tick + (uint32_t)it;
-    const uint32_t genv = (uint32_t)(A.env_offset + g.gid);
-    int action = (MODE == MODE_STEP) ? (g.valid ? A.actions[node] : 0) : argmax9(F.q);
-    if (MODE != MODE_STEP && eps > 0.0f) {
-      const float coin = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x);
-      if (coin < eps) {   // the action draw only runs on exploring envs
+    const uint32_t genv = (uint32_t)(A.env_offset + d.gid);
+    bool explore = false;
+    if (MODE != MODE_STEP && eps > 0.0f) explore = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
+    int action[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int agent = min(16 * ct + c, N - 1);
+      action[ct] = (MODE == MODE_STEP) ? (valid[ct] ? A.actions[node[ct]] : 0) : argmax9(F.q[ct]);
+      if (explore) {   // the action draw only runs on exploring envs
         const u32x4 wd = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
         const int j = agent & 3;
         const uint32_t word = j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w));
-        action = uniform_int(word, kActions);
+        action[ct] = uniform_int(word, kActions);
       }
     }
 
-    // ---- env.step (VMAS World.step + scenario reward).  The G lanes of a slot split the
-    //      partner pairs (lane q: partners q, q + G, ...; the contact branch runs once per
-    //      lane instead of once per partner), then every lane sums the forces in VMAS
-    //      order: 0 + u, obstacle pair, agent pairs in ascending partner index (SURVEY
-    //      a1-a3); -f(p_u - p_v) == f(p_v - p_u) bit for bit.  Scratch: the H/T/R rows,
-    //      free after the forward.
-    float* fb = &SW[w].H[0][0];
-    static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
+    // ---- env.step (VMAS World.step + scenario reward).  The 4 row groups of an agent
+    //      split its partner pairs (group p: partners p, p + 4, ...), then every lane sums
+    //      the forces in VMAS order: 0 + u, obstacle pair, agent pairs in ascending partner
+    //      index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
+    {   // pair mapping independent of the D layout: 64 / NS lanes per agent (NS = 8: one pair per lane)
+      constexpr int LPN = 64 / NS;
+      const int n = d.lane / LPN;
+      const float pxn = sm.px[n], pyn = sm.py[n];
 #pragma unroll
-    for (int j = 0; j < NS / Wpg<NS>::G; ++j) {
-      const int u = g.q + j * Wpg<NS>::G;
-      float gx = 0.0f, gy = 0.0f;
-      if (u < N) pair_force(px - sm.px[u], py - sm.py[u], gx, gy);   // u == agent: exactly 0
-      *reinterpret_cast<float2*>(fb + 2 * (g.s * NS + u)) = make_float2(gx, gy);
-    }
-    float fx = 0.0f + action_level(action / 3);
-    float fy = 0.0f + action_level(action % 3);
-    if (A.scenario == SWARM_OBSTACLE_AVOIDANCE) {
-      float gx, gy;
-      pair_force(px - kObstX, py - kObstY, gx, gy);
-      fx = fx + gx; fy = fy + gy;
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      if (u < N) {
-        const float2 f = *reinterpret_cast<const float2*>(fb + 2 * (g.s * NS + u));
-        fx = fx + f.x; fy = fy + f.y;
+      for (int j = 0; j < NS / LPN; ++j) {
+        const int u = d.lane % LPN + LPN * j;
+        float gx = 0.0f, gy = 0.0f;
+        if (u < N && n < N) pair_force(pxn - sm.px[u], pyn - sm.py[u], gx, gy);   // u == n: exactly 0
+        *reinterpret_cast<float2*>(fb + 2 * (n * NS + u)) = make_float2(gx, gy);
       }
     }
-    const StepOut o = integrate(px, py, vx, vy, fx, fy);
+    wave_lds_sync();
+    StepOut o[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = min(16 * ct + c, NS - 1);
+      float fx = 0.0f + action_level(action[ct] / 3);
+      float fy = 0.0f + action_level(action[ct] % 3);
+      if (A.scenario == SWARM_OBSTACLE_AVOIDANCE) {
+        float gx, gy;
+        pair_force(px[ct] - kObstX, py[ct] - kObstY, gx, gy);
+        fx = fx + gx; fy = fy + gy;
+      }
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        if (u < N) {
+          const float2 f = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + u));
+          fx = fx + f.x; fy = fy + f.y;
+        }
+      }
+      o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
+      if (16 * ct + c < NS && p == 0) { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }
+    }
     if (it == 0) SWARM_STAMP(3);
-    if (g.q == 0) { sm.aux[g.s] = o.dgoal; sm.aux2[g.s] = (o.dobs <= 0.2f) ? 1.0f : 0.0f; }
     wave_lds_sync();
     float dj[NS], hj[NS];
 #pragma unroll
@@ -188,76 +209,75 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
 #pragma unroll
     for (int j = 1; j < NS; ++j)
       if (j < N) { dsum = dsum + dj[j]; hsum = hsum + hj[j]; }
-    float rew;
+    float rg = 0.0f;
     if (A.scenario == SWARM_GOTO) {
-      rew = -dj[0];
+      rg = -dj[0];
 #pragma unroll
       for (int j = 1; j < NS; ++j)
-        if (j < N) rew = rew + (-dj[j]);   // go_to_position_scenario.py:112-113
-    } else {
-      rew = oa_reward(o.dgoal, o.dobs);
+        if (j < N) rg = rg + (-dj[j]);   // go_to_position_scenario.py:112-113
     }
     const float avg = dsum / (float)N;
     if (A.scenario == SWARM_GOTO) hsum = 0.0f;
 
-    if (MODE == MODE_TICK || MODE == MODE_STEP) {
-      if (MODE == MODE_TICK && A.out.q && g.valid) {
 #pragma unroll
-        for (int j = 0; j < (kActions + Wpg<NS>::G - 1) / Wpg<NS>::G; ++j) {
-          const int a = g.q + j * Wpg<NS>::G;
-          if (a < kActions) A.out.q[node * kActions + a] = sm.Q[g.s][a];
+    for (int ct = 0; ct < CT; ++ct) {
+      const float rew = (A.scenario == SWARM_GOTO) ? rg : oa_reward(o[ct].dgoal, o[ct].dobs);
+      const int n = 16 * ct + c;
+      if (valid[ct]) {   // the node's four row groups share its stores
+        if (MODE == MODE_TICK || MODE == MODE_STEP) {
+          if (MODE == MODE_TICK && A.out.q)
+            for (int a = p; a < kActions; a += 4) A.out.q[node[ct] * kActions + a] = sm.Q[n][a];
+          if (MODE == MODE_TICK && A.out.mult && A.graph != SWARM_GRAPH_DENSE)
+            for (int u = p; u < N; u += 4)
+              A.out.mult[((size_t)d.gid * N + u) * N + n] = (uint8_t)in_mult<NS>(u, n, N, A.graph, sm, nullptr, d.gid);
+          if (p == 0) {
+            if (A.out.actions) A.out.actions[node[ct]] = action[ct];
+            if (A.out.reward) A.out.reward[node[ct]] = rew;
+            if (n == 0) {
+              if (A.out.avg_dist) A.out.avg_dist[d.gid] = avg;
+              if (A.out.hits) A.out.hits[d.gid] = hsum;
+            }
+          } else if (MODE == MODE_TICK && A.replay.s) {
+            const size_t ri = ((size_t)slot * A.B + d.gid) * N + n;
+            if (p == 1) reinterpret_cast<float4*>(A.replay.s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+            else if (p == 2) reinterpret_cast<float4*>(A.replay.s_next)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
+            else { A.replay.r[ri] = rew; A.replay.a[ri] = (uint8_t)action[ct]; }
+          }
+          if (p == 3 && A.out.obs) {
+            float* ob = A.out.obs + node[ct] * 6;
+            ob[0] = o[ct].px; ob[1] = o[ct].py; ob[2] = o[ct].vx; ob[3] = o[ct].vy; ob[4] = kGoalX; ob[5] = kGoalY;
+          }
+        } else if (p == 0) {  // MODE_ROLLOUT
+          if (A.out.traj_pos) {
+            const size_t ti = ((size_t)it * A.B + d.gid) * N + n;
+            reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o[ct].px, o[ct].py);
+          }
+          if (n == 0) {
+            if (A.out.traj_dist) A.out.traj_dist[(size_t)it * A.B + d.gid] = avg;
+            if (A.out.traj_hits) A.out.traj_hits[(size_t)it * A.B + d.gid] = hsum;
+          }
         }
       }
-      if (writer) {
-        if (A.out.actions) A.out.actions[node] = action;
-        if (A.out.reward) A.out.reward[node] = rew;
-        if (MODE == MODE_TICK && A.replay.s) {
-          const size_t ri = ((size_t)slot * A.B + g.gid) * N + agent;
-          reinterpret_cast<float4*>(A.replay.s)[ri] = make_float4(px, py, vx, vy);
-          reinterpret_cast<float4*>(A.replay.s_next)[ri] = make_float4(o.px, o.py, o.vx, o.vy);
-          A.replay.r[ri] = rew;
-          A.replay.a[ri] = (uint8_t)action;
-        }
-        if (agent == 0) {
-          if (A.out.avg_dist) A.out.avg_dist[g.gid] = avg;
-          if (A.out.hits) A.out.hits[g.gid] = hsum;
-        }
-      }
-      if (MODE == MODE_TICK && A.out.mult && A.graph != SWARM_GRAPH_DENSE && g.valid) {
-        int mult[NS];
-        in_edges<NS>(g, N, A.graph, sm, nullptr, mult);
-        for (int u = g.q; u < N; u += Wpg<NS>::G) A.out.mult[((size_t)g.gid * N + u) * N + agent] = (uint8_t)mult[u];
-      }
-    } else if (writer) {  // MODE_ROLLOUT
-      if (A.out.traj_pos) {
-        const size_t ti = ((size_t)it * A.B + g.gid) * N + agent;
-        reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o.px, o.py);
-      }
-      if (agent == 0) {
-        if (A.out.traj_dist) A.out.traj_dist[(size_t)it * A.B + g.gid] = avg;
-        if (A.out.traj_hits) A.out.traj_hits[(size_t)it * A.B + g.gid] = hsum;
-      }
+      rew_sum[ct] = rew_sum[ct] + rew;
+      px[ct] = o[ct].px; py[ct] = o[ct].py; vx[ct] = o[ct].vx; vy[ct] = o[ct].vy;
     }
-    rew_sum = rew_sum + rew;
     hits_sum = hits_sum + hsum;
-    px = o.px; py = o.py; vx = o.vx; vy = o.vy;
-    if ((MODE == MODE_TICK || MODE == MODE_STEP) && writer && A.out.obs) {
-      float* ob = A.out.obs + node * 6;
-      ob[0] = px; ob[1] = py; ob[2] = vx; ob[3] = vy; ob[4] = kGoalX; ob[5] = kGoalY;
-    }
-    if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && writer && agent == 0) {
-      if (A.out.avg_dist) A.out.avg_dist[g.gid] = avg;
-      if (A.out.hits) A.out.hits[g.gid] = hits_sum;
+    if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && c == 0 && p == 0 && d.live) {
+      if (A.out.avg_dist) A.out.avg_dist[d.gid] = avg;
+      if (A.out.hits) A.out.hits[d.gid] = hits_sum;
     }
     wave_lds_sync();   // every lane done with this tick's LDS rows before the next tick rewrites them
   }
-  if (writer) {
-    reinterpret_cast<float4*>(A.state)[node] = make_float4(px, py, vx, vy);
-    if (MODE == MODE_ROLLOUT) {
-      if (A.out.reward) A.out.reward[node] = rew_sum;
-      if (A.out.obs) {
-        float* ob = A.out.obs + node * 6;
-        ob[0] = px; ob[1] = py; ob[2] = vx; ob[3] = vy; ob[4] = kGoalX; ob[5] = kGoalY;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    if (valid[ct] && p == 0) {
+      reinterpret_cast<float4*>(A.state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+      if (MODE == MODE_ROLLOUT) {
+        if (A.out.reward) A.out.reward[node[ct]] = rew_sum[ct];
+        if (A.out.obs) {
+          float* ob = A.out.obs + node[ct] * 6;
+          ob[0] = px[ct]; ob[1] = py[ct]; ob[2] = vx[ct]; ob[3] = vy[ct]; ob[4] = kGoalX; ob[5] = kGoalY;
+        }
       }
     }
   }

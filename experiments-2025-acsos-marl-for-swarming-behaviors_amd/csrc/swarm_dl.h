@@ -1,0 +1,327 @@
+// swarm_dl.h — GCN.forward of one graph per wave entirely in the MFMA 16x16x4 f32
+// accumulator layout ("D layout", swarm_wpg.h): lane l -> column c = l & 15 (a node
+// slot: node n = 16 ct + c of column tile ct) and row group p = l >> 4; register
+// (t, r) of a 32-wide per-node vector is hidden feature 16 t + 4 p + r.
+//
+// Every dense product is an MFMA whose B operand is the previous stage's registers:
+//   conv1.lin   H^T = W X^T            (K = 7 -> 2 k-steps; X straight from the state)
+//   aggregate   O^T = H^T C^T          (K = NS source slots; C = attention coefficients)
+//   lin1        Z^T = W1 tanh(O)^T     (K = 32; k-step (t, r) <-> feature 16 t + 4 p + r)
+//   lin2        Q^T = W2 relu(Z)^T
+// Per-node scalars (attention scores) are partial dot products reduced over the four
+// row groups with permlane swaps; node-to-node data (scores, positions, the H rows the
+// aggregation reads, Q rows) goes through wave-private LDS with wave-scope syncs.
+//
+// GCN.forward: src/training/train_gcn_dqn.py:59-70 (GATConv -> tanh -> lin1 -> relu
+// -> lin2); GATConv math: PyG 2.5.3 (heads 1, add_self_loops False).
+#pragma once
+#include "swarm_wpg.h"
+
+namespace swarm {
+
+// sum over the four row groups (lanes l, l^16, l^32, l^48), bitwise identical in all four
+__device__ inline float row4_sum(float x) {
+  const int xi = __float_as_int(x);
+  const auto a = __builtin_amdgcn_permlane16_swap(xi, xi, false, false);
+  const float y = __int_as_float((int)a[0]) + __int_as_float((int)a[1]);
+  const int yi = __float_as_int(y);
+  const auto b = __builtin_amdgcn_permlane32_swap(yi, yi, false, false);
+  return __int_as_float((int)b[0]) + __int_as_float((int)b[1]);
+}
+
+// pick v[4 k + p] for this lane's row group p (register arrays cannot be indexed by lane)
+template <int M>
+__device__ inline float pick4(const float (&v)[M], int k, int p) {
+  const float a = v[4 * k], b = v[4 * k + 1], c = v[4 * k + 2], d = v[4 * k + 3];
+  return p == 0 ? a : (p == 1 ? b : (p == 2 ? c : d));
+}
+
+template <int NS>
+struct DGeom {
+  static constexpr int CT = (NS + 15) / 16;   // column tiles of 16 node slots
+  int lane, c, p;
+  int gid;      // env (acting) or batch index (TD) of this wave; 0 if idle
+  bool live;
+};
+
+template <int NS>
+__device__ inline DGeom<NS> make_dgeom(int wave_gid, int count) {
+  DGeom<NS> d;
+  d.lane = threadIdx.x & 63;
+  d.c = d.lane & 15;
+  d.p = d.lane >> 4;
+  d.live = wave_gid < count;
+  d.gid = d.live ? wave_gid : 0;
+  return d;
+}
+
+// per-lane forward state; index ct = column tile (node n = 16 ct + c)
+template <int NS>
+struct DFwd {
+  static constexpr int CT = DGeom<NS>::CT;
+  float x[CT][2];            // X[n][p], X[n][4 + p] (features: px py vx vy gx gy id 0)
+  float t[CT][2][4];         // tanh(conv out)
+  float zr[CT][2][4];        // relu(lin1)
+  float cf[CT][NS];          // attention coefficient of the in-edge u -> n (0 if none)
+  float sdst[CT];            // destination score of n
+  float q[CT][kActions];     // Q row of n
+};
+
+// features of node n for this lane's two k-slots (p, 4 + p) from its state (pos, vel)
+__device__ inline void node_x(float px, float py, float vx, float vy, int agent, int p, float x[2]) {
+  x[0] = p == 0 ? px : (p == 1 ? py : (p == 2 ? vx : vy));
+  x[1] = p == 0 ? kGoalX : (p == 1 ? kGoalY : (p == 2 ? (float)agent : 0.0f));
+}
+
+// multiplicity m(u -> n) (complete: train_gcn_dqn.py:101-108; kNN: simulator.py:15-24;
+// dense: caller-supplied [B][N][N])
+template <int NS>
+__device__ inline int in_mult(int u, int n, int N, int graph, const WSmall<NS>& sm, const uint8_t* __restrict__ dense,
+                              int gid) {
+  if (u >= N || n >= N) return 0;
+  if (graph == SWARM_GRAPH_COMPLETE) return (u != n ? 1 : 0) + ((u == 0 && n == 0) ? 1 : 0);
+  if (graph == SWARM_GRAPH_KNN)
+    return (int)((sm.knn[u] >> n) & 1u) + (int)((sm.knn[n] >> u) & 1u) + ((u == 0 && n == 0) ? 1 : 0);
+  return (int)dense[((size_t)gid * N + u) * N + n];
+}
+
+// kNN row of node n (positions in sm)
+template <int NS>
+__device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& sm) {
+  float d[NS];
+  const float xi = sm.px[n], yi = sm.py[n];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) d[j] = (j < N) ? norm2(sm.px[j] - xi, sm.py[j] - yi) : 0.0f;
+  return topk_smallest_mask<NS>(d, N, k);
+}
+
+// Full GCN.forward.  F.x must hold the lane's features (zero for nodes >= N).  P is the
+// padded LDS weight image.  Writes the H rows (and T / R rows if keep_tr) of V, the
+// per-node scalars of V.sm, and leaves F.t / F.zr / F.cf / F.q for the backward.
+template <int NS, int SB = -1>
+__device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& d, int N, int graph, int k, int conv,
+                                  const uint8_t* __restrict__ dense, const WView<NS>& V, bool keep_tr, DFwd<NS>& F) {
+#define DF_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
+  constexpr int CT = DGeom<NS>::CT;
+  WSmall<NS>& sm = *V.sm;
+  const int c = d.c, p = d.p;
+  // ---- conv1.lin on MFMA (K = 7 padded to 8): A[f][k] = W[f][k], B[k][n] = X[n][k]
+  float h[CT][2][4];
+  {
+    float a0[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a0[t][0] = P[L_W + (16 * t + c) * kFeat + p];
+      a0[t][1] = (4 + p < kFeat) ? P[L_W + (16 * t + c) * kFeat + 4 + p] : 0.0f;
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        acc = mfma16(a0[t][0], F.x[ct][0], acc);
+        acc = mfma16(a0[t][1], F.x[ct][1], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[ct][t][r] = acc[r];
+      }
+  }
+  // ---- attention scores (h * att).sum(-1): 8 features per lane, then the 4 row groups
+  float ssrc[CT];
+  {
+    const float4 s0 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 4 * p);
+    const float4 s1 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 16 + 4 * p);
+    const float4 d0 = *reinterpret_cast<const float4*>(P + L_ATT_DST + 4 * p);
+    const float4 d1 = *reinterpret_cast<const float4*>(P + L_ATT_DST + 16 + 4 * p);
+    const float as[2][4] = {{s0.x, s0.y, s0.z, s0.w}, {s1.x, s1.y, s1.z, s1.w}};
+    const float ad[2][4] = {{d0.x, d0.y, d0.z, d0.w}, {d1.x, d1.y, d1.z, d1.w}};
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      float ps = 0.0f, pd = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { ps = ps + h[ct][t][r] * as[t][r]; pd = pd + h[ct][t][r] * ad[t][r]; }
+      ssrc[ct] = row4_sum(ps);
+      F.sdst[ct] = row4_sum(pd);
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = 16 * ct + c;
+    if (n < NS) {
+      *reinterpret_cast<float4*>(&V.H[n][4 * p]) = make_float4(h[ct][0][0], h[ct][0][1], h[ct][0][2], h[ct][0][3]);
+      *reinterpret_cast<float4*>(&V.H[n][16 + 4 * p]) = make_float4(h[ct][1][0], h[ct][1][1], h[ct][1][2], h[ct][1][3]);
+      if (p == 0) { sm.ssrc[n] = ssrc[ct]; sm.sdst[n] = F.sdst[ct]; sm.px[n] = F.x[ct][0]; }
+      if (p == 1) sm.py[n] = F.x[ct][0];
+    }
+  }
+  wave_lds_sync();
+  DF_STAMP(0);
+  if (graph == SWARM_GRAPH_KNN) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c;
+      if (n < NS && p == 0) sm.knn[n] = (n < N) ? knn_mask_node<NS>(n, N, k, sm) : 0u;
+    }
+    wave_lds_sync();
+  }
+  // ---- in-edge coefficients of target n (every row group computes them; PyG softmax
+  //      exp(e - max) / (sum + 1e-16) with duplicate edges counted by multiplicity)
+  if (conv == SWARM_CONV_GAT) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c;
+      float e[NS];
+      int m[NS];
+      float emax = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        m[u] = in_mult<NS>(u, n, N, graph, sm, dense, d.gid);
+        e[u] = leaky(sm.ssrc[u] + F.sdst[ct]);
+        emax = m[u] > 0 ? fmaxf(emax, e[u]) : emax;
+      }
+      float den = 0.0f;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        e[u] = m[u] > 0 ? __expf(e[u] - emax) : 0.0f;
+        den = den + (float)m[u] * e[u];
+      }
+      den = den + 1e-16f;
+      const float inv = 1.0f / den;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) F.cf[ct][u] = (float)m[u] * (e[u] * inv);
+    }
+  } else {
+    // GCNConv (a13, parity unpinned): self loops collapse to weight 1, symmetric deg^-1/2
+    float dis[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c;
+      float deg = 0.0f;
+#pragma unroll
+      for (int u = 0; u < NS; ++u)
+        if (u < N) deg = deg + (u == n ? 1.0f : (float)in_mult<NS>(u, n, N, graph, sm, dense, d.gid));
+      dis[ct] = (n < N && deg > 0.0f) ? 1.0f / sqrtf(deg) : 0.0f;
+      if (n < NS && p == 0) sm.aux[n] = dis[ct];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const float w = (u == n) ? 1.0f : (float)in_mult<NS>(u, n, N, graph, sm, dense, d.gid);
+        F.cf[ct][u] = (u < N && n < N) ? (sm.aux[u] * w) * dis[ct] : 0.0f;
+      }
+    }
+  }
+  DF_STAMP(1);
+  // ---- aggregate on MFMA: O^T[f][n] = sum_u H[u][f] C[n][u], K = NS source slots
+  {
+    float ah[2][NS / 4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < NS / 4; ++ks) ah[t][ks] = V.H[4 * ks + p][16 * t + c];
+    const float4 b0 = *reinterpret_cast<const float4*>(P + L_BIAS + 4 * p);
+    const float4 b1 = *reinterpret_cast<const float4*>(P + L_BIAS + 16 + 4 * p);
+    const float bias[2][4] = {{b0.x, b0.y, b0.z, b0.w}, {b1.x, b1.y, b1.z, b1.w}};
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NS / 4; ++ks) {
+        const float b = pick4(F.cf[ct], ks, p);
+        o0 = mfma16(ah[0][ks], b, o0);
+        o1 = mfma16(ah[1][ks], b, o1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        F.t[ct][0][r] = tanh_fast(o0[r] + bias[0][r]);
+        F.t[ct][1][r] = tanh_fast(o1[r] + bias[1][r]);
+      }
+      const int n = 16 * ct + c;
+      if (keep_tr && n < NS) {
+        *reinterpret_cast<float4*>(&V.T[n][4 * p]) = make_float4(F.t[ct][0][0], F.t[ct][0][1], F.t[ct][0][2], F.t[ct][0][3]);
+        *reinterpret_cast<float4*>(&V.T[n][16 + 4 * p]) = make_float4(F.t[ct][1][0], F.t[ct][1][1], F.t[ct][1][2], F.t[ct][1][3]);
+      }
+    }
+  }
+  DF_STAMP(2);
+  // ---- lin1 + relu on MFMA: Z^T = W1 tanh^T, the tanh registers are the B operand
+  {
+    float a1[2][2][4];   // [out tile t2][k tile t][r] = W1[16 t2 + c][16 t + 4 p + r]
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float4 w = *reinterpret_cast<const float4*>(P + L_W1 + (16 * t2 + c) * kWRow + 16 * t + 4 * p);
+        a1[t2][t][0] = w.x; a1[t2][t][1] = w.y; a1[t2][t][2] = w.z; a1[t2][t][3] = w.w;
+      }
+    const float4 bb0 = *reinterpret_cast<const float4*>(P + L_B1 + 4 * p);
+    const float4 bb1 = *reinterpret_cast<const float4*>(P + L_B1 + 16 + 4 * p);
+    const float b1v[2][4] = {{bb0.x, bb0.y, bb0.z, bb0.w}, {bb1.x, bb1.y, bb1.z, bb1.w}};
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z = mfma16(a1[t2][t][r], F.t[ct][t][r], z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float u = z[r] + b1v[t2][r];
+          F.zr[ct][t2][r] = u > 0.0f ? u : 0.0f;
+        }
+      }
+      const int n = 16 * ct + c;
+      if (keep_tr && n < NS) {
+        *reinterpret_cast<float4*>(&V.R[n][4 * p]) = make_float4(F.zr[ct][0][0], F.zr[ct][0][1], F.zr[ct][0][2], F.zr[ct][0][3]);
+        *reinterpret_cast<float4*>(&V.R[n][16 + 4 * p]) = make_float4(F.zr[ct][1][0], F.zr[ct][1][1], F.zr[ct][1][2], F.zr[ct][1][3]);
+      }
+    }
+  }
+  DF_STAMP(3);
+  // ---- lin2 on MFMA: Q^T = W2 relu^T (A rows >= 9 zero); Q rows exchanged through LDS
+  {
+    float a2[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c < kActions) w = *reinterpret_cast<const float4*>(P + L_W2 + c * kWRow + 16 * t + 4 * p);
+      a2[t][0] = w.x; a2[t][1] = w.y; a2[t][2] = w.z; a2[t][3] = w.w;
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      f32x4 qa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qa = mfma16(a2[t][r], F.zr[ct][t][r], qa);
+      const int n = 16 * ct + c;
+      if (n < NS && p < 3) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = 4 * p + r;
+          if (a < kActions) sm.Q[n][a] = qa[r] + P[L_B2 + a];
+        }
+      }
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = min(16 * ct + c, NS - 1);
+    const float4 q0 = *reinterpret_cast<const float4*>(&sm.Q[n][0]);
+    const float4 q1 = *reinterpret_cast<const float4*>(&sm.Q[n][4]);
+    F.q[ct][0] = q0.x; F.q[ct][1] = q0.y; F.q[ct][2] = q0.z; F.q[ct][3] = q0.w;
+    F.q[ct][4] = q1.x; F.q[ct][5] = q1.y; F.q[ct][6] = q1.z; F.q[ct][7] = q1.w;
+    F.q[ct][8] = sm.Q[n][8];
+  }
+  DF_STAMP(4);
+#undef DF_STAMP
+}
+
+}  // namespace swarm

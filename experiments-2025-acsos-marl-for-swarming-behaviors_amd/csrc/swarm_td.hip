@@ -18,7 +18,7 @@
 #include <stdlib.h>
 
 #include "swarm_adam.h"
-#include "swarm_wpg.h"
+#include "swarm_dl.h"
 
 namespace swarm {
 
@@ -73,7 +73,7 @@ __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*B
 
 template <int NS>
 __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
-  constexpr int GPB = kTdRows / NS, G = Wpg<NS>::G, FPL = Wpg<NS>::FPL;
+  constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;
   constexpr int NT = 128 * GPB;
   __shared__ TdLds<NS> TB;
   __shared__ __attribute__((aligned(16))) float Pon[N_LDS_PARAMS];
@@ -82,11 +82,10 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   const bool online = wave < GPB;
   const int wi = online ? wave : wave - GPB;
   const int N = A.N;
-  const WGeom<NS> g = make_wgeom<NS>(blockIdx.x * GPB + wi, A.S, N);
-  const int row0 = wi * NS, row = row0 + g.s;
+  const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * GPB + wi, A.S);
+  const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
-  const int lane = g.lane;
-  const int agent = g.valid ? g.s : 0;
+  const int lane = d.lane, c = d.c, p = d.p;
   float* gslab = A.slabs + (size_t)blockIdx.x * (N_PARAMS + 1);
   SWARM_STAMP(0);
 
@@ -100,88 +99,91 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
   const uint32_t n_graphs = valid_slots * (uint32_t)A.B;
   if (n_graphs < (uint32_t)A.S) {
-    for (int p = threadIdx.x; p <= N_PARAMS; p += NT) gslab[p] = 0.0f;
+    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) gslab[q] = 0.0f;
     return;
   }
   // ---- sample (GraphReplayBuffer.sample: random.sample -> keyed permutation)
   uint32_t gid = 0;
   if (A.sample_in) {
-    gid = (uint32_t)A.sample_in[g.gid];
+    gid = (uint32_t)A.sample_in[d.gid];
   } else {
     const SampleKey sk = sample_key(n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, A.ctrl->tick);
-    gid = sample_index((uint32_t)g.gid, sk);
+    gid = sample_index((uint32_t)d.gid, sk);
   }
-  if (A.sample_out && online && g.live && lane == 0) A.sample_out[g.gid] = (int32_t)gid;
+  if (A.sample_out && online && d.live && lane == 0) A.sample_out[d.gid] = (int32_t)gid;
   SWARM_STAMP(1);
   const uint32_t slot = gid / (uint32_t)A.B, genv = gid % (uint32_t)A.B;
-  const size_t ri = ((size_t)slot * A.B + genv) * N + agent;
-  const float4 st = reinterpret_cast<const float4*>(online ? A.replay.s : A.replay.s_next)[ri];
-  const float rew = A.replay.r[ri];
-  const int act = g.valid ? (int)A.replay.a[ri] : 0;
+  float rew[CT];
+  int act[CT];
+  bool nv[CT];
+  DFwd<NS> F;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = 16 * ct + c;
+    nv[ct] = d.live && n < N;
+    const size_t ri = ((size_t)slot * A.B + genv) * N + min(n, N - 1);
+    const float4 st = reinterpret_cast<const float4*>(online ? A.replay.s : A.replay.s_next)[ri];
+    rew[ct] = A.replay.r[ri];
+    act[ct] = nv[ct] ? (int)A.replay.a[ri] : 0;
+    node_x(st.x, st.y, st.z, st.w, n, p, F.x[ct]);
+    if (!nv[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
+  }
   pon.store(Pon, threadIdx.x);
   ptg.store(Ptg, threadIdx.x);
-
-  WFwd<NS> F;
-  F.x[0] = st.x; F.x[1] = st.y; F.x[2] = st.z; F.x[3] = st.w;
-  F.x[4] = kGoalX; F.x[5] = kGoalY; F.x[6] = (float)agent; F.x[7] = 0.0f;
-  if (!g.valid) {
+  if (online && p == 0) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) F.x[k] = 0.0f;
+    for (int ct = 0; ct < CT; ++ct)
+      if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = act[ct];
   }
-  if (online && g.q == 0) TB.act[row] = act;
   __syncthreads();   // B0: weight images
   SWARM_STAMP(2);
-  // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121)
-  wpg_forward<NS, 16>(online ? Pon : Ptg, g, N, A.graph, A.k, A.conv, nullptr, V, F);
-  if (!online && g.q == 0) {
-    float qmax = F.q[0];
+  // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121).
+  //      Everything after B1 waits for the target waves' y, so they issue first.
+  if (!online) __builtin_amdgcn_s_setprio(2);
+  dl_forward<NS, 16>(online ? Pon : Ptg, d, N, A.graph, A.k, A.conv, nullptr, V, online, F);
+  if (!online && p == 0) {
 #pragma unroll
-    for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[a]);
-    TB.y[row] = rew + A.gamma * qmax;
+    for (int ct = 0; ct < CT; ++ct) {
+      float qmax = F.q[ct][0];
+#pragma unroll
+      for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[ct][a]);
+      if (16 * ct + c < NS) TB.y[row0 + 16 * ct + c] = nv[ct] ? rew[ct] + A.gamma * qmax : 0.0f;
+    }
   }
+  if (!online) __builtin_amdgcn_s_setprio(0);
   SWARM_STAMP(3);
   __syncthreads();   // B1: TD targets
   SWARM_STAMP(4);
 
   const float* P = Pon;
-  constexpr int CT = Dl<NS>::CT;
-  const int c = lane & 15, p = lane >> 4;
   float dz[CT][2][4];
   if (online) {
     // ---- dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ, dZ = dR * [z > 0]
-    //      in D layout: lane (c, p) handles node 16 ct + c, features 16 t + 4 p + r
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c, nn = min(n, NS - 1);
-      const bool nv = g.live && n < N;
-      const int an = TB.act[row0 + nn];
-      const float delta = nv ? (V.sm->Q[nn][an] - TB.y[row0 + nn]) : 0.0f;
+      float qa = F.q[ct][0];
+#pragma unroll
+      for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? F.q[ct][a] : qa;
+      const float delta = nv[ct] ? (qa - TB.y[row0 + nn]) : 0.0f;
       const float gq = delta * A.grad_scale;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const float4 w = *reinterpret_cast<const float4*>(P + L_W2 + an * kWRow + 16 * t + 4 * p);
+        const float4 w = *reinterpret_cast<const float4*>(P + L_W2 + act[ct] * kWRow + 16 * t + 4 * p);
         const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) dz[ct][t][r] = F.zr[ct][t][r] > 0.0f ? wv[r] * gq : 0.0f;
       }
       if (n < NS) {
-        *reinterpret_cast<float4*>(&TB.dZ[row0 + n][4 * p]) = make_float4(dz[ct][0][0], dz[ct][0][1], dz[ct][0][2], dz[ct][0][3]);
-        *reinterpret_cast<float4*>(&TB.dZ[row0 + n][16 + 4 * p]) = make_float4(dz[ct][1][0], dz[ct][1][1], dz[ct][1][2], dz[ct][1][3]);
-        if (p == 0) { TB.gq[row0 + n] = gq; TB.d2[row0 + n] = delta * delta; }
+        const int row = row0 + n;
+        *reinterpret_cast<float4*>(&TB.dZ[row][4 * p]) = make_float4(dz[ct][0][0], dz[ct][0][1], dz[ct][0][2], dz[ct][0][3]);
+        *reinterpret_cast<float4*>(&TB.dZ[row][16 + 4 * p]) = make_float4(dz[ct][1][0], dz[ct][1][1], dz[ct][1][2], dz[ct][1][3]);
+        TB.X[row][p] = F.x[ct][0];
+        TB.X[row][4 + p] = F.x[ct][1];
+#pragma unroll
+        for (int j = 0; j < NS / 4; ++j) TB.cm[row][4 * j + p] = pick4(F.cf[ct], j, p);
+        if (p == 0) { TB.X[row][8] = 0.0f; TB.gq[row] = gq; TB.d2[row] = delta * delta; }
       }
-    }
-    if (g.q == 0) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) TB.X[row][k] = k < kFeat ? F.x[k] : 0.0f;
-      TB.X[row][8] = 0.0f;
-    }
-    if (!g.valid) {
-#pragma unroll
-      for (int u = 0; u < NS; ++u) F.c[u] = 0.0f;
-    }
-    if (g.q == 0) {
-#pragma unroll
-      for (int u = 0; u < NS; ++u) TB.cm[row][u] = F.c[u];
     }
   }
   __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph
@@ -189,12 +191,12 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
 
   const int col = lane & 31, h = lane >> 5;
   if (online) {
-    // ---- dT^T[feature][node] = W1^T dZ^T on MFMA (k-step (t, r) -> k = 16 t + 4 p + r,
-    //      the dz registers are the B operand), dO = dT * (1 - t^2), D layout
+    // ---- dT^T = W1^T dZ^T on MFMA (the dz registers are the B operand),
+    //      dO = dT * (1 - t^2) with the forward's tanh registers
+    float dO[CT][2][4];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const int n = 16 * ct + c, nn = min(n, NS - 1);
-      const bool nv = g.live && n < N;
+      const int n = 16 * ct + c;
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -203,78 +205,122 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             acc = mfma16(P[L_W1 + (16 * t + 4 * p + r) * kWRow + 16 * t2 + c], dz[ct][t][r], acc);
-        const float4 tv = *reinterpret_cast<const float4*>(&TB.T[row0 + nn][16 * t2 + 4 * p]);
-        const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
-        float o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = nv ? acc[r] * (1.0f - tt[r] * tt[r]) : 0.0f;
-        if (n < NS) *reinterpret_cast<float4*>(&TB.dO[row0 + n][16 * t2 + 4 * p]) = make_float4(o[0], o[1], o[2], o[3]);
+        for (int r = 0; r < 4; ++r)
+          dO[ct][t2][r] = nv[ct] ? acc[r] * (1.0f - F.t[ct][t2][r] * F.t[ct][t2][r]) : 0.0f;
+      }
+      if (n < NS) {
+        *reinterpret_cast<float4*>(&TB.dO[row0 + n][4 * p]) = make_float4(dO[ct][0][0], dO[ct][0][1], dO[ct][0][2], dO[ct][0][3]);
+        *reinterpret_cast<float4*>(&TB.dO[row0 + n][16 + 4 * p]) = make_float4(dO[ct][1][0], dO[ct][1][1], dO[ct][1][2], dO[ct][1][3]);
       }
     }
-    wave_lds_sync();   // dO rows of this graph
-    float dO[FPL];
-    lds_load<FPL>(&TB.dO[row][g.f0], dO);
-    // ---- GAT backward (attention part), branch-free over the graph's sources u
-    float da_d = 0.0f;
+    SWARM_STAMP(24);
+    // ---- GAT backward (attention part).  g[u][v] = H_u . dO_v on MFMA (A = H rows,
+    //      B = the dO registers); lane (c, p) holds g[u = 16 ut + 4 p + r][v = 16 ct + c]
+    float da_d[CT];
+    WSmall<NS>& sm = *V.sm;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) da_d[ct] = 0.0f;
     if (A.conv == SWARM_CONV_GAT) {
-      float gu[NS];
+      float ah[CT][2][4];
 #pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        gu[u] = 0.0f;
-        if (u < N) {
-          float hv[FPL];
-          lds_load<FPL>(&TB.H[row0 + u][g.f0], hv);
-          float part = 0.0f;
+      for (int ut = 0; ut < CT; ++ut) {
+        const int u = min(16 * ut + c, NS - 1);
 #pragma unroll
-          for (int i = 0; i < FPL; ++i) part = part + dO[i] * hv[i];
-          gu[u] = slot_sum<G>(part);
+        for (int t = 0; t < 2; ++t) {
+          const float4 hv = *reinterpret_cast<const float4*>(&TB.H[row0 + u][16 * t + 4 * p]);
+          ah[ut][t][0] = hv.x; ah[ut][t][1] = hv.y; ah[ut][t][2] = hv.z; ah[ut][t][3] = hv.w;
         }
       }
-      float Gs = 0.0f;
 #pragma unroll
-      for (int u = 0; u < NS; ++u)
-        if (u < N) Gs = Gs + F.c[u] * gu[u];
-      WSmall<NS>& sm = *V.sm;
+      for (int ct = 0; ct < CT; ++ct) {
+        const int v = 16 * ct + c;
+        float gv[CT][4], cu[CT][4];
+        float part = 0.0f;
 #pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        float dpu = 0.0f;
-        if (u < N) {
-          const float de = F.c[u] * (gu[u] - Gs);
-          const float pre = sm.ssrc[u] + F.sdst;
-          dpu = pre > 0.0f ? de : de * kLeakySlope;
+        for (int ut = 0; ut < CT; ++ut) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc = mfma16(ah[ut][t][r], dO[ct][t][r], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // coefficient of edge u -> v, u = 16 ut + 4 p + r (registers hold every u of target v)
+            float cc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int uq = 16 * ut + 4 * q + r;
+              cc[q] = uq < NS ? F.cf[ct][uq < NS ? uq : 0] : 0.0f;
+            }
+            cu[ut][r] = p == 0 ? cc[0] : (p == 1 ? cc[1] : (p == 2 ? cc[2] : cc[3]));
+            gv[ut][r] = acc[r];
+            part = part + cu[ut][r] * gv[ut][r];
+          }
         }
-        da_d = da_d + dpu;
-        if (u < N && g.q == 0) TB.dp[row][u] = dpu;
+        const float Gs = row4_sum(part);
+        float dsum = 0.0f;
+#pragma unroll
+        for (int ut = 0; ut < CT; ++ut)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = 16 * ut + 4 * p + r;
+            float dpu = 0.0f;
+            if (u < N && nv[ct]) {
+              const float de = cu[ut][r] * (gv[ut][r] - Gs);
+              const float pre = sm.ssrc[u] + F.sdst[ct];
+              dpu = pre > 0.0f ? de : de * kLeakySlope;
+            }
+            dsum = dsum + dpu;
+            if (u < NS && v < NS) TB.dp[row0 + v][u] = dpu;
+          }
+        da_d[ct] = row4_sum(dsum);
       }
     }
-    wave_lds_sync();   // dp rows of this graph
-    float da_s = 0.0f;
-    if (A.conv == SWARM_CONV_GAT) {
+    wave_lds_sync();   // dp / dO rows of this graph
+    SWARM_STAMP(25);
+    // ---- dh_u = sum_v c[v][u] dO_v (MFMA: A = dO rows, B = C column) + da_src att_src + da_dst att_dst
+    const float4 s0 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 4 * p);
+    const float4 s1 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 16 + 4 * p);
+    const float4 d0 = *reinterpret_cast<const float4*>(P + L_ATT_DST + 4 * p);
+    const float4 d1 = *reinterpret_cast<const float4*>(P + L_ATT_DST + 16 + 4 * p);
+    const float as[2][4] = {{s0.x, s0.y, s0.z, s0.w}, {s1.x, s1.y, s1.z, s1.w}};
+    const float ad[2][4] = {{d0.x, d0.y, d0.z, d0.w}, {d1.x, d1.y, d1.z, d1.w}};
+    float ao[2][NS / 4];
 #pragma unroll
-      for (int v = 0; v < NS; ++v)
-        if (v < N) da_s = da_s + TB.dp[row0 + v][agent];
-    }
-    if (!g.valid) { da_s = 0.0f; da_d = 0.0f; }
-    // ---- dh = sum_v c[v][me] dO_v + da_src att_src + da_dst att_dst
-    float dh[FPL], as[FPL], ad[FPL];
-    lds_load<FPL>(P + L_ATT_SRC + g.f0, as);
-    lds_load<FPL>(P + L_ATT_DST + g.f0, ad);
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int i = 0; i < FPL; ++i) dh[i] = 0.0f;
+      for (int ks = 0; ks < NS / 4; ++ks) ao[t][ks] = TB.dO[row0 + 4 * ks + p][16 * t + c];
 #pragma unroll
-    for (int v = 0; v < NS; ++v) {
-      if (v < N) {
-        const float cv = g.valid ? TB.cm[row0 + v][agent] : 0.0f;   // c[target v][source me]
-        float dv[FPL];
-        lds_load<FPL>(&TB.dO[row0 + v][g.f0], dv);
+    for (int ct = 0; ct < CT; ++ct) {
+      const int u = 16 * ct + c, uu = min(u, NS - 1);
+      float da_s = 0.0f;
+      if (A.conv == SWARM_CONV_GAT) {
 #pragma unroll
-        for (int i = 0; i < FPL; ++i) dh[i] = dh[i] + cv * dv[i];
+        for (int v = 0; v < NS; ++v)
+          if (v < N) da_s = da_s + TB.dp[row0 + v][uu];
+      }
+      const float das = nv[ct] ? da_s : 0.0f, dad = nv[ct] ? da_d[ct] : 0.0f;
+      f32x4 m0 = {0.f, 0.f, 0.f, 0.f}, m1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NS / 4; ++ks) {
+        const float b = TB.cm[row0 + 4 * ks + p][uu];
+        m0 = mfma16(ao[0][ks], b, m0);
+        m1 = mfma16(ao[1][ks], b, m1);
+      }
+      float dh[2][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dh[0][r] = nv[ct] ? (m0[r] + das * as[0][r]) + dad * ad[0][r] : 0.0f;
+        dh[1][r] = nv[ct] ? (m1[r] + das * as[1][r]) + dad * ad[1][r] : 0.0f;
+      }
+      if (u < NS) {
+        *reinterpret_cast<float4*>(&TB.dH[row0 + u][4 * p]) = make_float4(dh[0][0], dh[0][1], dh[0][2], dh[0][3]);
+        *reinterpret_cast<float4*>(&TB.dH[row0 + u][16 + 4 * p]) = make_float4(dh[1][0], dh[1][1], dh[1][2], dh[1][3]);
+        if (p == 0) { TB.das[row0 + u] = das; TB.dad[row0 + u] = dad; }
       }
     }
-#pragma unroll
-    for (int i = 0; i < FPL; ++i) dh[i] = (dh[i] + da_s * as[i]) + da_d * ad[i];
-    lds_store<FPL>(&TB.dH[row][g.f0], dh);
-    if (g.q == 0) { TB.das[row] = da_s; TB.dad[row] = da_d; }
+    SWARM_STAMP(27);
   } else {
     // ---- target waves: products that need only B2's images
     //      job 0: dW1 = dZ^T T ; job 1: dW2 = onehot(a) gq R, db2, loss ; job 2: db1
@@ -296,20 +342,24 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
           const int a = acc_row(r, h);
           if (a < kActions) gslab[OFF_W2 + a * kHidden + col] = dW2[r];
         }
-        if (lane < kActions) {
-          float s_b2 = 0.0f;
-          for (int n = 0; n < kTdRows; ++n) s_b2 = s_b2 + (TB.act[n] == lane ? TB.gq[n] : 0.0f);
-          gslab[OFF_B2 + lane] = s_b2;
-        } else if (lane == 63) {
-          float s_loss = 0.0f;
-          for (int n = 0; n < kTdRows; ++n) s_loss = s_loss + TB.d2[n];
-          gslab[N_PARAMS] = s_loss;
+        if (lane < kActions || lane == 63) {   // every read issued before the ordered sum
+          float v[kTdRows];
+#pragma unroll
+          for (int n = 0; n < kTdRows; ++n) v[n] = lane == 63 ? TB.d2[n] : (TB.act[n] == lane ? TB.gq[n] : 0.0f);
+          float acc = v[0];
+#pragma unroll
+          for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+          gslab[lane == 63 ? N_PARAMS : OFF_B2 + lane] = acc;
         }
       } else {
         if (lane < kHidden) {
-          float s_b1 = 0.0f;
-          for (int n = 0; n < kTdRows; ++n) s_b1 = s_b1 + TB.dZ[n][lane];
-          gslab[OFF_B1 + lane] = s_b1;
+          float v[kTdRows];
+#pragma unroll
+          for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
+          float acc = v[0];
+#pragma unroll
+          for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+          gslab[OFF_B1 + lane] = acc;
         }
       }
     }
@@ -330,20 +380,24 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) gslab[OFF_W + acc_row(r, h) * kFeat + col] = dW[r];
       }
-    } else if (job == 4) {
-      float s_a = 0.0f;
-      if (h == 0) {
-        for (int n = 0; n < kTdRows; ++n) s_a = s_a + TB.das[n] * TB.H[n][col];
-        gslab[OFF_ATT_SRC + col] = s_a;
-      } else {
-        for (int n = 0; n < kTdRows; ++n) s_a = s_a + TB.dad[n] * TB.H[n][col];
-        gslab[OFF_ATT_DST + col] = s_a;
-      }
+    } else if (job == 4) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
+      const float* da = h == 0 ? TB.das : TB.dad;
+      float v[kTdRows];
+#pragma unroll
+      for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
+      float acc = v[0];
+#pragma unroll
+      for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+      gslab[(h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col] = acc;
     } else {
       if (lane < kHidden) {
-        float s_bias = 0.0f;
-        for (int n = 0; n < kTdRows; ++n) s_bias = s_bias + TB.dO[n][lane];
-        gslab[OFF_BIAS + lane] = s_bias;
+        float v[kTdRows];
+#pragma unroll
+        for (int n = 0; n < kTdRows; ++n) v[n] = TB.dO[n][lane];
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        gslab[OFF_BIAS + lane] = acc;
       }
     }
   }

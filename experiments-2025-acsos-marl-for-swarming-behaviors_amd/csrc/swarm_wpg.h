@@ -128,19 +128,6 @@ struct WScratch {
   __device__ WView<NS> view() { return WView<NS>{H, T, R, &sm}; }
 };
 
-// per-lane activations of the forward that the TD backward re-uses
-template <int NS>
-struct WFwd {
-  static constexpr int FPL = Wpg<NS>::FPL;
-  float x[8];          // node features (k < 7)
-  float h[FPL];        // conv1.lin output
-  float t[FPL];        // tanh(conv out)
-  float zr[(NS + 15) / 16][2][4];   // relu(lin1) in D layout (see mfma16 below)
-  float q[kActions];   // Q row of this lane's slot (every lane of the slot)
-  float sdst;          // destination score of this slot
-  float c[NS];         // coefficient of the in-edge u -> s (multiplicity x attention), 0 if none
-};
-
 template <int K>
 __device__ inline void lds_load(const float* __restrict__ p, float* out) {   // K floats, 16-B aligned
 #pragma unroll
@@ -203,187 +190,6 @@ __device__ inline void in_edges(const WGeom<NS>& g, int N, int graph, const WSma
     }
     mult[u] = m;
   }
-}
-
-// Full GCN.forward of the wave's graph.  F.x must hold this slot's features.  P is
-// the padded LDS weight image (lds_index).  Writes H/T/R rows and the per-slot
-// scalars of V; every lane ends with F.q, and F.zr holds relu(lin1) in D layout.
-template <int NS, int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
-__device__ inline void wpg_forward(const float* __restrict__ P, const WGeom<NS>& g, int N, int graph, int k,
-                                   int conv, const uint8_t* __restrict__ dense, const WView<NS>& V, WFwd<NS>& F) {
-#define WF_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
-  constexpr int G = Wpg<NS>::G, FPL = Wpg<NS>::FPL;
-  WSmall<NS>& sm = *V.sm;
-  const int s = g.s, f0 = g.f0;
-  // ---- conv1.lin (no bias): h = W x, K = 7
-  {
-    float w[FPL * kFeat];
-    lds_load<FPL * kFeat>(P + L_W + f0 * kFeat, w);
-#pragma unroll
-    for (int i = 0; i < FPL; ++i) {
-      float a = w[i * kFeat] * F.x[0];
-#pragma unroll
-      for (int kk = 1; kk < kFeat; ++kk) a = fmaf(w[i * kFeat + kk], F.x[kk], a);
-      F.h[i] = a;
-    }
-  }
-  // ---- attention scores: (h * att).sum(-1)
-  float ssrc;
-  {
-    float as[FPL], ad[FPL];
-    lds_load<FPL>(P + L_ATT_SRC + f0, as);
-    lds_load<FPL>(P + L_ATT_DST + f0, ad);
-    float ps = 0.0f, pd = 0.0f;
-#pragma unroll
-    for (int i = 0; i < FPL; ++i) { ps = ps + F.h[i] * as[i]; pd = pd + F.h[i] * ad[i]; }
-    ssrc = slot_sum<G>(ps);
-    F.sdst = slot_sum<G>(pd);
-  }
-  WF_STAMP(0);
-  lds_store<FPL>(&V.H[s][f0], F.h);
-  if (g.q == 0) { sm.ssrc[s] = ssrc; sm.sdst[s] = F.sdst; sm.px[s] = F.x[0]; sm.py[s] = F.x[1]; }
-  wave_lds_sync();
-  if (graph == SWARM_GRAPH_KNN) {
-    const uint32_t m = g.valid ? knn_mask<NS>(g, N, k, sm) : 0u;
-    if (g.q == 0) sm.knn[s] = m;
-    wave_lds_sync();
-  }
-  int mult[NS];
-  in_edges<NS>(g, N, graph, sm, dense, mult);
-  WF_STAMP(1);
-  // ---- attention softmax over in-edges (PyG softmax: exp(e - max) / (sum + 1e-16)),
-  //      duplicate edges counted by multiplicity; branch-free over the sources
-  if (conv == SWARM_CONV_GAT) {
-    float e[NS];
-    float emax = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const bool on = (u < N) && mult[u] > 0;
-      e[u] = leaky(sm.ssrc[u < N ? u : 0] + F.sdst);
-      emax = on ? fmaxf(emax, e[u]) : emax;
-    }
-    float den = 0.0f;
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const bool on = (u < N) && mult[u] > 0;
-      e[u] = on ? __expf(e[u] - emax) : 0.0f;
-      den = den + (float)mult[u] * e[u];
-    }
-    den = den + 1e-16f;
-    const float inv = 1.0f / den;
-#pragma unroll
-    for (int u = 0; u < NS; ++u) F.c[u] = (float)mult[u] * (e[u] * inv);
-  } else {
-    // GCNConv (a13, parity unpinned): self loops collapse to weight 1, symmetric deg^-1/2
-    float deg = 0.0f;
-#pragma unroll
-    for (int u = 0; u < NS; ++u)
-      if (u < N) deg = deg + (u == s ? 1.0f : (float)mult[u]);
-    const float dis = deg > 0.0f ? 1.0f / sqrtf(deg) : 0.0f;
-    if (g.q == 0) sm.aux[s] = g.valid ? dis : 0.0f;
-    wave_lds_sync();
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      F.c[u] = 0.0f;
-      if (u < N && g.valid) F.c[u] = (sm.aux[u] * (u == s ? 1.0f : (float)mult[u])) * dis;
-    }
-  }
-  WF_STAMP(2);
-  // ---- aggregate + bias + tanh
-  {
-    float out[FPL], b[FPL];
-#pragma unroll
-    for (int i = 0; i < FPL; ++i) out[i] = 0.0f;
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      if (u < N) {   // uniform; c[u] == 0 for non-edges
-        float hv[FPL];
-        lds_load<FPL>(&V.H[u][f0], hv);
-#pragma unroll
-        for (int i = 0; i < FPL; ++i) out[i] = out[i] + F.c[u] * hv[i];
-      }
-    }
-    lds_load<FPL>(P + L_BIAS + f0, b);
-#pragma unroll
-    for (int i = 0; i < FPL; ++i) F.t[i] = tanh_fast(out[i] + b[i]);
-  }
-  WF_STAMP(3);
-  lds_store<FPL>(&V.T[s][f0], F.t);
-  wave_lds_sync();
-  // ---- lin1 + relu on MFMA: Z^T[feature][node] = W1 T^T, K = 32 in 8 k-steps of 4
-  //      (k-step s pairs k-slot p with k = 4 s + p)
-  const int c = g.lane & 15, p = g.lane >> 4;
-  {
-    float a1[2][8];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) a1[t][ks] = P[L_W1 + (16 * t + c) * kWRow + 4 * ks + p];
-    const float4 b1a = *reinterpret_cast<const float4*>(P + L_B1 + 4 * p);
-    const float4 b1b = *reinterpret_cast<const float4*>(P + L_B1 + 16 + 4 * p);
-    const float b1v[2][4] = {{b1a.x, b1a.y, b1a.z, b1a.w}, {b1b.x, b1b.y, b1b.z, b1b.w}};
-#pragma unroll
-    for (int ct = 0; ct < Dl<NS>::CT; ++ct) {
-      const int n = min(16 * ct + c, NS - 1);   // columns past NS: clamped reads, results unused
-      f32x4 z0 = {0.f, 0.f, 0.f, 0.f}, z1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const float b = V.T[n][4 * ks + p];
-        z0 = mfma16(a1[0][ks], b, z0);
-        z1 = mfma16(a1[1][ks], b, z1);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float u0 = z0[r] + b1v[0][r], u1 = z1[r] + b1v[1][r];
-        F.zr[ct][0][r] = u0 > 0.0f ? u0 : 0.0f;
-        F.zr[ct][1][r] = u1 > 0.0f ? u1 : 0.0f;
-      }
-      if (16 * ct + c < NS) {   // natural-order R row (TD products)
-        *reinterpret_cast<float4*>(&V.R[16 * ct + c][4 * p]) =
-            make_float4(F.zr[ct][0][0], F.zr[ct][0][1], F.zr[ct][0][2], F.zr[ct][0][3]);
-        *reinterpret_cast<float4*>(&V.R[16 * ct + c][16 + 4 * p]) =
-            make_float4(F.zr[ct][1][0], F.zr[ct][1][1], F.zr[ct][1][2], F.zr[ct][1][3]);
-      }
-    }
-  }
-  WF_STAMP(4);
-  // ---- lin2 on MFMA: Q^T[action][node] = W2 R^T; the relu registers are the B operand
-  //      (k-step (t, r) -> k = 16 t + 4 p + r); A rows >= 9 are zero
-  {
-    float a2[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (c < kActions) w = *reinterpret_cast<const float4*>(P + L_W2 + c * kWRow + 16 * t + 4 * p);
-      a2[t][0] = w.x; a2[t][1] = w.y; a2[t][2] = w.z; a2[t][3] = w.w;
-    }
-#pragma unroll
-    for (int ct = 0; ct < Dl<NS>::CT; ++ct) {
-      f32x4 qa = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) qa = mfma16(a2[t][r], F.zr[ct][t][r], qa);
-      const int n = 16 * ct + c;
-      if (n < NS && p < 3) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int a = 4 * p + r;
-          if (a < kActions) sm.Q[n][a] = qa[r] + P[L_B2 + a];
-        }
-      }
-    }
-  }
-  wave_lds_sync();
-  {
-    const float4 q0 = *reinterpret_cast<const float4*>(&sm.Q[s][0]);
-    const float4 q1 = *reinterpret_cast<const float4*>(&sm.Q[s][4]);
-    F.q[0] = q0.x; F.q[1] = q0.y; F.q[2] = q0.z; F.q[3] = q0.w;
-    F.q[4] = q1.x; F.q[5] = q1.y; F.q[6] = q1.z; F.q[7] = q1.w;
-    F.q[8] = sm.Q[s][8];
-  }
-  WF_STAMP(5);
-#undef WF_STAMP
 }
 
 }  // namespace swarm

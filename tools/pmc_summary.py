@@ -1,0 +1,56 @@
+"""Summarise the rocprofv3 --pmc passes of prof_pmc.sh into per-kernel medians and the
+HBM traffic per launch that bench.py's roofline reports.
+
+FETCH_SIZE / WRITE_SIZE are in KB per dispatch; on gfx950 FETCH_SIZE reports half the
+bytes of a wide coalesced read, so it is doubled (MI355X_MICROARCH.md §HBM).  Both count
+Infinity-Cache hits, so the figure is fabric traffic below L2, an upper bound on HBM.
+
+usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc_td.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+KERNELS = {"td": "td_kernel", "act": "act_kernel<8, 1>", "reduce": "grad_reduce_kernel"}
+
+
+def main(src, dst):
+    vals = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(src, "p*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            for key, pat in KERNELS.items():
+                if pat in r["Kernel_Name"]:
+                    vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    out = {"source": "rocprofv3 --kernel-trace --pmc, four separate passes (prof_pmc.sh), bench.py workload",
+           "units": "counter medians per dispatch; *_bytes in bytes",
+           "kernels": {}}
+    for key in KERNELS:
+        k = {c: statistics.median(v) for (kk, c), v in vals.items() if kk == key}
+        if not k:
+            continue
+        fetch = 2.0 * k.get("FETCH_SIZE", 0.0) * 1024.0
+        write = k.get("WRITE_SIZE", 0.0) * 1024.0
+        waves = k.get("SQ_WAVES", 0.0) or 1.0
+        out["kernels"][key] = {
+            "counters": k,
+            "fetch_bytes_corrected": fetch,
+            "write_bytes": write,
+            "hbm_bytes_per_launch": fetch + write,
+            "per_wave": {c: k[c] / waves for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA",
+                                                    "SQ_WAVE_CYCLES", "SQ_WAIT_ANY") if c in k},
+        }
+    if "td" in out["kernels"]:
+        out["hbm_bytes_per_launch"] = out["kernels"]["td"]["hbm_bytes_per_launch"]
+    json.dump(out, open(dst, "w"), indent=1)
+    for key, v in out["kernels"].items():
+        print(f"{key:7s} fetch {v['fetch_bytes_corrected'] / 1e3:8.1f} KB  write {v['write_bytes'] / 1e3:8.1f} KB  "
+              f"per wave: " + ", ".join(f"{c.replace('SQ_', '')} {x:.0f}" for c, x in v["per_wave"].items()))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc", sys.argv[2] if len(sys.argv) > 2 else
+         "profiles/r01_pmc_td.json")

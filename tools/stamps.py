@@ -15,8 +15,8 @@ import torch  # noqa: E402
 import swarm_amd  # noqa: E402
 from swarm_amd import _lib  # noqa: E402
 
-FWD = {0: "fwd lin0 + scores", 1: "fwd H/scalars -> LDS, in-edges", 2: "fwd softmax",
-       3: "fwd aggregate + tanh", 4: "fwd T exchange + lin1", 5: "fwd R exchange + lin2 + Q exchange"}
+FWD = {0: "fwd lin0 + scores + H image", 1: "fwd softmax coefficients", 2: "fwd aggregate MFMA + tanh",
+       3: "fwd lin1 MFMA", 4: "fwd lin2 MFMA + Q exchange"}
 ACT = {0: "entry", 20: "pro: loads issued + ctrl", 21: "pro: norm partials (data arrival)",
        22: "pro: norm reduction (barrier)", 23: "pro: Adam elements", 24: "pro: w -> LDS",
        1: "pro: barrier", **{8 + k: v for k, v in FWD.items()},
@@ -24,13 +24,18 @@ ACT = {0: "entry", 20: "pro: loads issued + ctrl", 21: "pro: norm partials (data
        3: "eps-greedy + physics", 4: "reward/metrics + stores"}
 TD = {0: "entry", 1: "params loads + ctrl + skip + sample index", 2: "replay loads + LDS stage + barrier",
       **{16 + k: v for k, v in FWD.items()}, 3: "(y)", 4: "barrier (y ready)", 5: "dQ/dZ images + barrier",
-      6: "dT/dO/GAT bwd/dh | dW1,dW2,b1 products + barrier", 7: "dW / att / bias products"}
+      24: "bwd: dT MFMA + dO images", 25: "bwd: GAT g MFMA / dp + sync",
+      27: "bwd: da_src + dh messages MFMA + dH images",
+      6: "(online: B3 barrier) | target: dW1,dW2,b1 products + B3", 7: "dW / att / bias products"}
 
 
-def report(buf, names, nwaves):
+ACT_ORDER = [0, 20, 21, 22, 23, 24, 1, 8, 9, 10, 11, 12, 2, 3, 4]
+TD_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 24, 25, 27, 6, 7]
+
+
+def report(buf, names, nwaves, order):
     a = buf.reshape(-1, 32)[:nwaves].astype(np.int64)
-    order = sorted(names, key=lambda k: (k if k < 8 else (1.5 + (k - 8) * 0.01 if k < 16 else (2.5 + (k - 16) * 0.01 if k < 20 else 0.5 + (k - 20) * 0.01))))
-    order = [k for k in order if (a[:, k] > 0).all()]
+    order = [k for k in order if k in names and (a[:, k] > 0).all()]
     tot = np.median(a[:, order[-1]] - a[:, order[0]])
     print(f"  total median {tot:.0f} cycles")
     for p, k in zip(order, order[1:]):
@@ -58,15 +63,15 @@ def main():
     torch.cuda.synchronize()
     ab = (B + 3) // 4
     print(f"act_kernel ({ab} blocks x 4 waves, one env per wave):")
-    report(sa.cpu().numpy()[: ab * 16 * 32].reshape(ab, 16, 32)[:, :4].reshape(-1), ACT, ab * 4)
+    report(sa.cpu().numpy()[: ab * 16 * 32].reshape(ab, 16, 32)[:, :4].reshape(-1), ACT, ab * 4, ACT_ORDER)
     ns = 8 if N <= 8 else (16 if N <= 16 else 32)
     gpb = 32 // ns
     blocks = (B + gpb - 1) // gpb
     td = st.cpu().numpy()[: blocks * 16 * 32].reshape(blocks, 16, 32)
     print(f"td_kernel ({blocks} blocks x {gpb} graphs), online waves:")
-    report(td[:, :gpb].reshape(-1), TD, blocks * gpb)
+    report(td[:, :gpb].reshape(-1), TD, blocks * gpb, TD_ORDER)
     print("td_kernel target waves:")
-    report(td[:, gpb:2 * gpb].reshape(-1), TD, blocks * gpb)
+    report(td[:, gpb:2 * gpb].reshape(-1), TD, blocks * gpb, TD_ORDER)
 
 
 if __name__ == "__main__":
