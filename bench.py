@@ -148,33 +148,28 @@ def main():
     ctrl = eng.read_ctrl()
     assert ctrl["trained"] == 1 and math.isfinite(ctrl["loss"]), ctrl
 
-    # ---- per-kernel durations with HIP events on the launch stream (eager ticks)
+    # ---- per-kernel durations: each kernel of the fused tick as a captured chain of KCHAIN
+    #      back-to-back launches (the same inputs every launch: TD and the slab reduce are pure
+    #      functions of them; the act launch re-applies the same pending step and advances the
+    #      envs), replayed with HIP events recorded on the stream the graph launches on.
+    #      Back-to-back launches are what the rocprofv3 kernel trace of this command times.
     kt = {}
     if not args.no_kernel_timing:
         stream = torch.cuda.current_stream()
-        names = ("swarm_act_step", "swarm_td_grad", "swarm_adam_step")
-        acc = {n: [] for n in names}
-        for _ in range(min(args.steps, 50)):
-            if tick_in_ep[0] >= max_steps:
-                eng.reset()
-                tick_in_ep[0] = 0
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-            ev[0].record(stream)
-            eng.act(push=True, full_out=False)
-            ev[1].record(stream)
-            ev[2].record(stream)
-            eng.td_grad()
-            ev[3].record(stream)
-            eng.allreduce_grad()
-            ev[4].record(stream)
-            eng.adam()
-            ev[5].record(stream)
-            tick_in_ep[0] += 1
-            torch.cuda.synchronize()
-            acc["swarm_act_step"].append(ev[0].elapsed_time(ev[1]) * 1e3)
-            acc["swarm_td_grad"].append(ev[2].elapsed_time(ev[3]) * 1e3)
-            acc["swarm_adam_step"].append(ev[4].elapsed_time(ev[5]) * 1e3)
-        kt = {n: float(np.mean(v)) for n, v in acc.items()}   # microseconds (td_grad includes grad_reduce)
+        kchain = 50
+        for name, fn in (("td_kernel", eng.launch_td), ("act_kernel", eng.launch_train_act),
+                         ("grad_reduce_kernel", eng.launch_grad_reduce)):
+            fn()
+            g = eng.capture(kchain, fn)
+            per = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                g.replay()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                per.append(e0.elapsed_time(e1) * 1e3 / kchain)
+            kt[name] = float(np.median(per))   # microseconds per launch
 
     value = B * N * world * args.steps / elapsed
     ms = elapsed / args.steps * 1e3
@@ -183,7 +178,7 @@ def main():
     td_flops_launch = S * N * (2 * f_fwd + td_bwd_flops(N, d))
     roof = None
     if kt:
-        t_td = kt["swarm_td_grad"] * 1e-6
+        t_td = kt["td_kernel"] * 1e-6
         ach = td_flops_launch / t_td / 1e12
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "r01_pmc_td.json")

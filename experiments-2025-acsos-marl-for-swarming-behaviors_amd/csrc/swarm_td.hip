@@ -89,29 +89,24 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   float* gslab = A.slabs + (size_t)blockIdx.x * (N_PARAMS + 1);
   SWARM_STAMP(0);
 
-  // ---- weights: both images' loads issued first (one round trip)
+  // ---- fused tick: this wave's replay indices come from the previous launch, so the
+  //      dependent pair (index -> replay rows) is issued first and the weight staging and
+  //      ctrl reads overlap it.  Indices are clamped into the ring: a skipped tick reads
+  //      valid (unused) rows.
+  const uint32_t cap = (uint32_t)A.replay.capacity;
+  const uint32_t ring_graphs = cap * (uint32_t)A.B;
+  uint32_t gid = 0;
+  if (A.sample_in) gid = min((uint32_t)A.sample_in[d.gid], ring_graphs - 1u);
   ParamStage<NT> pon, ptg;
   pon.load(A.params, threadIdx.x);
   ptg.load(A.target, threadIdx.x);
-  // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
   const uint32_t filled = A.ctrl->filled_slots;
-  const uint32_t cap = (uint32_t)A.replay.capacity;
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
   const uint32_t n_graphs = valid_slots * (uint32_t)A.B;
-  if (n_graphs < (uint32_t)A.S) {
-    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) gslab[q] = 0.0f;
-    return;
-  }
-  // ---- sample (GraphReplayBuffer.sample: random.sample -> keyed permutation)
-  uint32_t gid = 0;
-  if (A.sample_in) {
-    gid = (uint32_t)A.sample_in[d.gid];
-  } else {
+  if (!A.sample_in) {   // GraphReplayBuffer.sample: random.sample -> keyed permutation
     const SampleKey sk = sample_key(n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, A.ctrl->tick);
-    gid = sample_index((uint32_t)d.gid, sk);
+    gid = n_graphs >= (uint32_t)A.S ? sample_index((uint32_t)d.gid, sk) : 0u;
   }
-  if (A.sample_out && online && d.live && lane == 0) A.sample_out[d.gid] = (int32_t)gid;
-  SWARM_STAMP(1);
   const uint32_t slot = gid / (uint32_t)A.B, genv = gid % (uint32_t)A.B;
   float rew[CT];
   int act[CT];
@@ -128,6 +123,13 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
     node_x(st.x, st.y, st.z, st.w, n, p, F.x[ct]);
     if (!nv[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
   }
+  // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
+  if (n_graphs < (uint32_t)A.S) {
+    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) gslab[q] = 0.0f;
+    return;
+  }
+  if (A.sample_out && online && d.live && lane == 0) A.sample_out[d.gid] = (int32_t)gid;
+  SWARM_STAMP(1);
   pon.store(Pon, threadIdx.x);
   ptg.store(Ptg, threadIdx.x);
   if (online && p == 0) {

@@ -244,6 +244,21 @@ class SwarmEngine:
         self.act(push=True, full_out=full_out)
         self.td_update()
 
+    # single launches of the fused tick (bench.py times each kernel as a back-to-back chain)
+    def launch_train_act(self):
+        check(self.lib.swarm_train_act_step(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
+                                            ptr(self.state), ctypes_ref(self.replay), ptr(self.ctrl),
+                                            ctypes_ref(self.out_min), stream_ptr()), "swarm_train_act_step")
+
+    def launch_td(self):
+        check(self.lib.swarm_td_grad(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.w_nxt), ptr(self.target),
+                                     ctypes_ref(self.replay), ptr(self.ctrl), ptr(self.samples), None,
+                                     ptr(self.slabs), stream_ptr()), "swarm_td_grad")
+
+    def launch_grad_reduce(self):
+        check(self.lib.swarm_grad_reduce(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
+                                         ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
+
     def train_tick(self, full_out: bool = False):
         """Fused training tick: 3 launches (+ an RCCL all-reduce when world_size > 1)."""
         cfg, hp = ctypes_ref(self.cfg), ctypes_ref(self.hp)
