@@ -199,7 +199,8 @@ def test_gpu_reproduces_recorded_reference_actions(sw, golden_weights, trajector
 
 # ------------------------------------------------------------------ fused acting tick
 @pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
-@pytest.mark.parametrize("N,graph,k", [(8, "complete", 0), (12, "knn", 10), (5, "knn", 5)])
+@pytest.mark.parametrize("N,graph,k", [(8, "complete", 0), (12, "knn", 10), (5, "knn", 5), (20, "complete", 0),
+                                      (29, "knn", 6)])
 def test_act_tick_parity(sw, golden_weights, scen, N, graph, k):
     B = 150
     p = _params(golden_weights, scen, 7)
@@ -256,13 +257,17 @@ def _fill_replay(eng, seed):
     eng.ctrl[1] = 0
 
 
-@pytest.mark.parametrize("scen,N,S", [("go_to", 8, 32), ("obstacle_avoidance", 12, 40), ("go_to", 5, 7), ("go_to", 8, 256)])
-def test_td_update_parity(sw, golden_weights, scen, N, S):
+@pytest.mark.parametrize("scen,N,S,graph,k", [("go_to", 8, 32, "complete", 0), ("obstacle_avoidance", 12, 40, "complete", 0),
+                                                ("go_to", 5, 7, "complete", 0), ("go_to", 8, 256, "complete", 0),
+                                                ("go_to", 20, 9, "complete", 0), ("obstacle_avoidance", 29, 5, "complete", 0),
+                                                ("obstacle_avoidance", 12, 24, "knn", 5), ("go_to", 20, 6, "knn", 10)])
+def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k):
     B = 16
     cap = max(4, -(-S // B))
     p = _params(golden_weights, scen, 5)
     tgt = _params(golden_weights, scen, 6)
-    eng = sw.SwarmEngine(scen, N, B, seed=2, params=p, batch=S, replay_capacity=cap * B, update_target_every=1000)
+    eng = sw.SwarmEngine(scen, N, B, seed=2, params=p, batch=S, replay_capacity=cap * B, update_target_every=1000,
+                         graph=graph, knn_k=max(k, 1))
     eng.target.copy_(tgt.cuda())
     _fill_replay(eng, S)
     idx = torch.randperm(cap * B, generator=torch.Generator().manual_seed(S))[:S].to(torch.int32)
@@ -273,7 +278,11 @@ def test_td_update_parity(sw, golden_weights, scen, N, S):
     s1 = eng.rep_s1.cpu()[slot, env]
     a = eng.rep_a.cpu()[slot, env].long()
     r = eng.rep_r.cpu()[slot, env]
-    ref = O.td_step(p, tgt, torch.zeros_like(p), torch.zeros_like(p), 0, s, a, r, s1)
+    ei = ein = None
+    if graph == "knn":   # per-graph kNN edge lists (simulator.py:15-24), offset like Batch.from_data_list
+        ei = torch.cat([O.knn_edge_index(s[g, :, :2], k) + g * N for g in range(S)], dim=1)
+        ein = torch.cat([O.knn_edge_index(s1[g, :, :2], k) + g * N for g in range(S)], dim=1)
+    ref = O.td_step(p, tgt, torch.zeros_like(p), torch.zeros_like(p), 0, s, a, r, s1, edge_index=ei, edge_index_next=ein)
     grad = eng.grad.cpu()
     loss = grad[O.N_PARAMS].item() / (S * N)
     assert_close_rel(loss, ref["loss"], 1e-5, "TD loss")
