@@ -74,31 +74,59 @@ __device__ inline void node_x(float px, float py, float vx, float vy, int agent,
 }
 
 // multiplicity m(u -> n) (complete: train_gcn_dqn.py:101-108; kNN: simulator.py:15-24;
-// dense: caller-supplied [B][N][N])
-template <int NS>
+// dense: caller-supplied [B][N][N]).  A wave holds NS / GS graphs of GS slots each;
+// slots of different graphs are never connected.
+template <int NS, int GS = NS>
 __device__ inline int in_mult(int u, int n, int N, int graph, const WSmall<NS>& sm, const uint8_t* __restrict__ dense,
                               int gid) {
-  if (u >= N || n >= N) return 0;
-  if (graph == SWARM_GRAPH_COMPLETE) return (u != n ? 1 : 0) + ((u == 0 && n == 0) ? 1 : 0);
+  if constexpr (GS < NS) {
+    if (u / GS != n / GS) return 0;
+  }
+  const int ju = (GS < NS) ? u % GS : u, jn = (GS < NS) ? n % GS : n;   // columns past NS: jn >= N
+  if (ju >= N || jn >= N) return 0;
+  if (graph == SWARM_GRAPH_COMPLETE) return (ju != jn ? 1 : 0) + ((ju == 0 && jn == 0) ? 1 : 0);
   if (graph == SWARM_GRAPH_KNN)
-    return (int)((sm.knn[u] >> n) & 1u) + (int)((sm.knn[n] >> u) & 1u) + ((u == 0 && n == 0) ? 1 : 0);
-  return (int)dense[((size_t)gid * N + u) * N + n];
+    return (int)((sm.knn[u] >> jn) & 1u) + (int)((sm.knn[n] >> ju) & 1u) + ((ju == 0 && jn == 0) ? 1 : 0);
+  return (int)dense[((size_t)gid * N + ju) * N + jn];
 }
 
-// kNN row of node n (positions in sm)
-template <int NS>
+// all in-edge multiplicities of target n, m[j] for source base + j (base = first slot of
+// n's graph); the graph-type switch is taken once and each case is branch-free
+template <int NS, int GS = NS>
+__device__ inline void in_mults(int n, int N, int graph, const WSmall<NS>& sm, const uint8_t* __restrict__ dense,
+                                int gid, int m[GS]) {
+  const int jn = (GS < NS) ? n % GS : n;
+  const int base = (GS < NS) ? (n / GS) * GS : 0;
+  const bool tv = jn < N;
+  if (graph == SWARM_GRAPH_COMPLETE) {
+#pragma unroll
+    for (int j = 0; j < GS; ++j) m[j] = (tv && j < N) ? (int)(j != jn) + (int)(j == 0 && jn == 0) : 0;
+  } else if (graph == SWARM_GRAPH_KNN) {
+    const uint32_t kn = sm.knn[min(n, NS - 1)];
+#pragma unroll
+    for (int j = 0; j < GS; ++j)
+      m[j] = (tv && j < N) ? (int)((sm.knn[base + j] >> jn) & 1u) + (int)((kn >> j) & 1u) + (int)(j == 0 && jn == 0) : 0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < GS; ++j) m[j] = (tv && j < N) ? (int)dense[((size_t)gid * N + j) * N + jn] : 0;
+  }
+}
+
+// kNN row of slot n over its graph (positions in sm; bit j = local node j)
+template <int NS, int GS = NS>
 __device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& sm) {
-  float d[NS];
+  float d[GS];
+  const int base = (GS < NS) ? (n / GS) * GS : 0;
   const float xi = sm.px[n], yi = sm.py[n];
 #pragma unroll
-  for (int j = 0; j < NS; ++j) d[j] = (j < N) ? norm2(sm.px[j] - xi, sm.py[j] - yi) : 0.0f;
-  return topk_smallest_mask<NS>(d, N, k);
+  for (int j = 0; j < GS; ++j) d[j] = (j < N) ? norm2(sm.px[base + j] - xi, sm.py[base + j] - yi) : 0.0f;
+  return topk_smallest_mask<GS>(d, N, k);
 }
 
 // Full GCN.forward.  F.x must hold the lane's features (zero for nodes >= N).  P is the
 // padded LDS weight image.  Writes the H rows (and T / R rows if keep_tr) of V, the
 // per-node scalars of V.sm, and leaves F.t / F.zr / F.cf / F.q for the backward.
-template <int NS, int SB = -1>
+template <int NS, int SB = -1, int GS = NS>
 __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& d, int N, int graph, int k, int conv,
                                   const uint8_t* __restrict__ dense, const WView<NS>& V, bool keep_tr, DFwd<NS>& F) {
 #define DF_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
@@ -161,7 +189,7 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c;
-      if (n < NS && p == 0) sm.knn[n] = (n < N) ? knn_mask_node<NS>(n, N, k, sm) : 0u;
+      if (n < NS && p == 0) sm.knn[n] = (((GS < NS) ? n % GS : n) < N) ? knn_mask_node<NS, GS>(n, N, k, sm) : 0u;
     }
     wave_lds_sync();
   }
@@ -170,38 +198,42 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
   if (conv == SWARM_CONV_GAT) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const int n = 16 * ct + c;
-      float e[NS];
-      int m[NS];
+      const int n = 16 * ct + c, base = (GS < NS) ? (n / GS) * GS : 0;
+      float e[GS];
+      int m[GS];
+      in_mults<NS, GS>(n, N, graph, sm, dense, d.gid, m);
       float emax = -INFINITY;
 #pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        m[u] = in_mult<NS>(u, n, N, graph, sm, dense, d.gid);
-        e[u] = leaky(sm.ssrc[u] + F.sdst[ct]);
-        emax = m[u] > 0 ? fmaxf(emax, e[u]) : emax;
+      for (int j = 0; j < GS; ++j) {
+        e[j] = leaky(sm.ssrc[base + j] + F.sdst[ct]);
+        emax = m[j] > 0 ? fmaxf(emax, e[j]) : emax;
       }
       float den = 0.0f;
 #pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        e[u] = m[u] > 0 ? __expf(e[u] - emax) : 0.0f;
-        den = den + (float)m[u] * e[u];
+      for (int j = 0; j < GS; ++j) {
+        e[j] = m[j] > 0 ? __expf(e[j] - emax) : 0.0f;
+        den = den + (float)m[j] * e[j];
       }
       den = den + 1e-16f;
       const float inv = 1.0f / den;
+      float cl[GS];
 #pragma unroll
-      for (int u = 0; u < NS; ++u) F.cf[ct][u] = (float)m[u] * (e[u] * inv);
+      for (int j = 0; j < GS; ++j) cl[j] = (float)m[j] * (e[j] * inv);
+#pragma unroll
+      for (int u = 0; u < NS; ++u) F.cf[ct][u] = (GS == NS || u / GS == n / GS) ? cl[u % GS] : 0.0f;
     }
   } else {
     // GCNConv (a13, parity unpinned): self loops collapse to weight 1, symmetric deg^-1/2
     float dis[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const int n = 16 * ct + c;
+      const int n = 16 * ct + c, base = (GS < NS) ? (n / GS) * GS : 0;
       float deg = 0.0f;
 #pragma unroll
-      for (int u = 0; u < NS; ++u)
-        if (u < N) deg = deg + (u == n ? 1.0f : (float)in_mult<NS>(u, n, N, graph, sm, dense, d.gid));
-      dis[ct] = (n < N && deg > 0.0f) ? 1.0f / sqrtf(deg) : 0.0f;
+      for (int j = 0; j < GS; ++j)
+        if (j < N) deg = deg + (base + j == n ? 1.0f : (float)in_mult<NS, GS>(base + j, n, N, graph, sm, dense, d.gid));
+      const int jn = (GS < NS) ? n % GS : n;
+      dis[ct] = (jn < N && deg > 0.0f) ? 1.0f / sqrtf(deg) : 0.0f;
       if (n < NS && p == 0) sm.aux[n] = dis[ct];
     }
     wave_lds_sync();
@@ -210,8 +242,10 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
       const int n = 16 * ct + c;
 #pragma unroll
       for (int u = 0; u < NS; ++u) {
-        const float w = (u == n) ? 1.0f : (float)in_mult<NS>(u, n, N, graph, sm, dense, d.gid);
-        F.cf[ct][u] = (u < N && n < N) ? (sm.aux[u] * w) * dis[ct] : 0.0f;
+        const bool same = (GS == NS) || (u / GS == n / GS);
+        const float w = (u == n) ? 1.0f : (float)in_mult<NS, GS>(u, n, N, graph, sm, dense, d.gid);
+        const int ju = (GS < NS) ? u % GS : u, jn = (GS < NS) ? n % GS : n;
+        F.cf[ct][u] = (same && ju < N && jn < N) ? (sm.aux[u] * w) * dis[ct] : 0.0f;
       }
     }
   }

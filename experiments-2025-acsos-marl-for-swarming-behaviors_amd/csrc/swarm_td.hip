@@ -71,9 +71,12 @@ __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*B
   return acc;
 }
 
-template <int NS>
+// NS node slots per wave holding NS / GS graphs of GS slots (GS = 8 < NS = 16 packs two
+// N <= 8 graphs into one wave: every MFMA column is a real node, one wave per SIMD).
+template <int NS, int GS>
 __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
-  constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;
+  constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;   // GPB: online (= target) waves per block
+  constexpr int GPW = NS / GS;                             // graphs per wave
   constexpr int NT = 128 * GPB;
   __shared__ TdLds<NS> TB;
   __shared__ __attribute__((aligned(16))) float Pon[N_LDS_PARAMS];
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   const bool online = wave < GPB;
   const int wi = online ? wave : wave - GPB;
   const int N = A.N;
-  const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * GPB + wi, A.S);
+  const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * GPB + wi, 1 << 30);   // lane geometry; liveness is per graph
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
   const int lane = d.lane, c = d.c, p = d.p;
@@ -95,8 +98,21 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   //      valid (unused) rows.
   const uint32_t cap = (uint32_t)A.replay.capacity;
   const uint32_t ring_graphs = cap * (uint32_t)A.B;
-  uint32_t gid = 0;
-  if (A.sample_in) gid = min((uint32_t)A.sample_in[d.gid], ring_graphs - 1u);
+  int sid[CT];     // batch index of this lane's graph
+  bool live[CT], nv[CT];
+  int jl[CT];      // local node index inside the graph
+  uint32_t gid[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = 16 * ct + c;
+    const int gi = (GS < NS) ? n / GS : 0;
+    jl[ct] = (GS < NS) ? n % GS : n;
+    sid[ct] = blockIdx.x * (kTdRows / GS) + wi * GPW + gi;
+    live[ct] = sid[ct] < A.S && n < NS;
+    nv[ct] = live[ct] && jl[ct] < N;
+    gid[ct] = 0;
+    if (A.sample_in) gid[ct] = min((uint32_t)A.sample_in[min(sid[ct], A.S - 1)], ring_graphs - 1u);
+  }
   ParamStage<NT> pon, ptg;
   pon.load(A.params, threadIdx.x);
   ptg.load(A.target, threadIdx.x);
@@ -105,22 +121,21 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   const uint32_t n_graphs = valid_slots * (uint32_t)A.B;
   if (!A.sample_in) {   // GraphReplayBuffer.sample: random.sample -> keyed permutation
     const SampleKey sk = sample_key(n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, A.ctrl->tick);
-    gid = n_graphs >= (uint32_t)A.S ? sample_index((uint32_t)d.gid, sk) : 0u;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      gid[ct] = n_graphs >= (uint32_t)A.S ? sample_index((uint32_t)min(sid[ct], A.S - 1), sk) : 0u;
   }
-  const uint32_t slot = gid / (uint32_t)A.B, genv = gid % (uint32_t)A.B;
   float rew[CT];
   int act[CT];
-  bool nv[CT];
   DFwd<NS> F;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
-    const int n = 16 * ct + c;
-    nv[ct] = d.live && n < N;
-    const size_t ri = ((size_t)slot * A.B + genv) * N + min(n, N - 1);
+    const uint32_t slot = gid[ct] / (uint32_t)A.B, genv = gid[ct] % (uint32_t)A.B;
+    const size_t ri = ((size_t)slot * A.B + genv) * N + min(jl[ct], N - 1);
     const float4 st = reinterpret_cast<const float4*>(online ? A.replay.s : A.replay.s_next)[ri];
     rew[ct] = A.replay.r[ri];
     act[ct] = nv[ct] ? (int)A.replay.a[ri] : 0;
-    node_x(st.x, st.y, st.z, st.w, n, p, F.x[ct]);
+    node_x(st.x, st.y, st.z, st.w, jl[ct], p, F.x[ct]);
     if (!nv[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
   }
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
@@ -128,7 +143,11 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
     for (int q = threadIdx.x; q <= N_PARAMS; q += NT) gslab[q] = 0.0f;
     return;
   }
-  if (A.sample_out && online && d.live && lane == 0) A.sample_out[d.gid] = (int32_t)gid;
+  if (A.sample_out && online && p == 0) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      if (live[ct] && jl[ct] == 0) A.sample_out[sid[ct]] = (int32_t)gid[ct];
+  }
   SWARM_STAMP(1);
   pon.store(Pon, threadIdx.x);
   ptg.store(Ptg, threadIdx.x);
@@ -142,7 +161,7 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121).
   //      Everything after B1 waits for the target waves' y, so they issue first.
   if (!online) __builtin_amdgcn_s_setprio(2);
-  dl_forward<NS, 16>(online ? Pon : Ptg, d, N, A.graph, A.k, A.conv, nullptr, V, online, F);
+  dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, A.graph, A.k, A.conv, nullptr, V, online, F);
   if (!online && p == 0) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
@@ -268,7 +287,7 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
           for (int r = 0; r < 4; ++r) {
             const int u = 16 * ut + 4 * p + r;
             float dpu = 0.0f;
-            if (u < N && nv[ct]) {
+            if (u < NS && cu[ut][r] != 0.0f && nv[ct]) {   // in-edges only (cross-graph / absent: c = 0)
               const float de = cu[ut][r] * (gv[ut][r] - Gs);
               const float pre = sm.ssrc[u] + F.sdst[ct];
               dpu = pre > 0.0f ? de : de * kLeakySlope;
@@ -297,10 +316,11 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
     for (int ct = 0; ct < CT; ++ct) {
       const int u = 16 * ct + c, uu = min(u, NS - 1);
       float da_s = 0.0f;
-      if (A.conv == SWARM_CONV_GAT) {
+      if (A.conv == SWARM_CONV_GAT) {   // sum over the targets v of u's own graph
+        const int base = (GS < NS) ? (uu / GS) * GS : 0;
 #pragma unroll
-        for (int v = 0; v < NS; ++v)
-          if (v < N) da_s = da_s + TB.dp[row0 + v][uu];
+        for (int j = 0; j < GS; ++j)
+          if (j < N) da_s = da_s + TB.dp[row0 + base + j][uu];
       }
       const float das = nv[ct] ? da_s : 0.0f, dad = nv[ct] ? da_d[ct] : 0.0f;
       f32x4 m0 = {0.f, 0.f, 0.f, 0.f}, m1 = {0.f, 0.f, 0.f, 0.f};
@@ -614,9 +634,9 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.grad_scale = (float)(2.0 / ((double)hp->batch * (double)cfg->n_agents));
   const int nb = td_blocks(cfg, hp->batch);
   hipStream_t st = (hipStream_t)stream;
-  if (a.N <= 8) hipLaunchKernelGGL((td_kernel<8>), dim3(nb), dim3(128 * 4), 0, st, a);
-  else if (a.N <= 16) hipLaunchKernelGGL((td_kernel<16>), dim3(nb), dim3(128 * 2), 0, st, a);
-  else hipLaunchKernelGGL((td_kernel<32>), dim3(nb), dim3(128), 0, st, a);
+  if (a.N <= 8) hipLaunchKernelGGL((td_kernel<16, 8>), dim3(nb), dim3(128 * 2), 0, st, a);
+  else if (a.N <= 16) hipLaunchKernelGGL((td_kernel<16, 16>), dim3(nb), dim3(128 * 2), 0, st, a);
+  else hipLaunchKernelGGL((td_kernel<32, 32>), dim3(nb), dim3(128), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -33,15 +33,18 @@ struct Wpg {
 // the first LDS write and none sits behind a branch (clamped index): one round trip.
 template <int NT>
 struct ParamStage {
+  // native 4-wide vectors: whole-float4 copies of HIP's float4 class lower to memcpys that
+  // SROA leaves in scratch / promoted LDS once NJ > 1
+  typedef float v4 __attribute__((ext_vector_type(4)));
   static constexpr int NF4 = N_PARAMS / 4;            // 418 full float4 (floats 0..1671)
   static constexpr int NJ = (NF4 + NT - 1) / NT;
-  float4 v[NJ];
+  v4 v[NJ];
   float tail;
   __device__ inline void load(const float* __restrict__ g, int tid) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int i = min(tid + j * NT, NF4 - 1);
-      v[j] = reinterpret_cast<const float4*>(g)[i];
+      v[j] = *reinterpret_cast<const v4*>(g + 4 * i);
     }
     tail = g[N_PARAMS - 1];
   }
@@ -50,7 +53,7 @@ struct ParamStage {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int i = tid + j * NT;
-      if (i < NF4) *reinterpret_cast<float4*>(lds + lds_index(4 * i)) = v[j];
+      if (i < NF4) *reinterpret_cast<v4*>(lds + lds_index(4 * i)) = v[j];
     }
     if (tid == 0) lds[lds_index(N_PARAMS - 1)] = tail;
   }

@@ -64,11 +64,12 @@ def main():
     ab = (B + 3) // 4
     print(f"act_kernel ({ab} blocks x 4 waves, one env per wave):")
     report(sa.cpu().numpy()[: ab * 16 * 32].reshape(ab, 16, 32)[:, :4].reshape(-1), ACT, ab * 4, ACT_ORDER)
-    ns = 8 if N <= 8 else (16 if N <= 16 else 32)
-    gpb = 32 // ns
-    blocks = (B + gpb - 1) // gpb
+    ns = 16 if N <= 16 else 32          # node slots per TD wave (two 8-slot graphs when N <= 8)
+    gs = 8 if N <= 8 else ns
+    gpb = 32 // ns                      # online (= target) waves per block
+    blocks = (B + 32 // gs - 1) // (32 // gs)
     td = st.cpu().numpy()[: blocks * 16 * 32].reshape(blocks, 16, 32)
-    print(f"td_kernel ({blocks} blocks x {gpb} graphs), online waves:")
+    print(f"td_kernel ({blocks} blocks x {gpb} online + {gpb} target waves), online waves:")
     report(td[:, :gpb].reshape(-1), TD, blocks * gpb, TD_ORDER)
     print("td_kernel target waves:")
     report(td[:, gpb:2 * gpb].reshape(-1), TD, blocks * gpb, TD_ORDER)
