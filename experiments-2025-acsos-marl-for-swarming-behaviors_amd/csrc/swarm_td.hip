@@ -388,31 +388,34 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   }
   __syncthreads();   // B3: dO / dH / das / dad
   SWARM_STAMP(6);
-  // ---- products over B3's images: job 3: dW = dH^T X ; job 4: att sums ; job 5: dbias
-  //      online waves take jobs 3, 4 ; target waves job 5
-  for (int job = online ? 3 + wi : 5 + wi; job < (online ? 5 : 6); job += GPB) {
-    if (job == 3) {
-      f32x16 dW = {};
+  // ---- products over B3's images, spread over all 2 GPB waves of the block:
+  //      job 0 / 1: dW rows 0-15 / 16-31 = sum_n dH[n][f] X[n][k] (MFMA 16x16x4, K = node rows)
+  //      job 2: att_src / att_dst (lane halves) ; job 3: dbias
+  {
+    const int wall = online ? wi : GPB + wi;
+    for (int job = wall; job < 4; job += 2 * GPB) {
+      if (job < 2) {
+        const int t = job;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int n = 2 * s + h;
-        dW = mfma32(TB.dH[n][col], col < 8 ? TB.X[n][col] : 0.0f, dW);
-      }
-      if (col < kFeat) {
+        for (int ks = 0; ks < kTdRows / 4; ++ks) {
+          const int n = 4 * ks + p;
+          acc = mfma16(TB.dH[n][16 * t + c], c < kFeat ? TB.X[n][c] : 0.0f, acc);
+        }
+        if (c < kFeat) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) gslab[OFF_W + acc_row(r, h) * kFeat + col] = dW[r];
-      }
-    } else if (job == 4) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
-      const float* da = h == 0 ? TB.das : TB.dad;
-      float v[kTdRows];
+          for (int r = 0; r < 4; ++r) gslab[OFF_W + (16 * t + 4 * p + r) * kFeat + c] = acc[r];
+        }
+      } else if (job == 2) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
+        const float* da = h == 0 ? TB.das : TB.dad;
+        float v[kTdRows];
 #pragma unroll
-      for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
-      float acc = v[0];
+        for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
+        float acc = v[0];
 #pragma unroll
-      for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-      gslab[(h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col] = acc;
-    } else {
-      if (lane < kHidden) {
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        gslab[(h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col] = acc;
+      } else if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = TB.dO[n][lane];
