@@ -73,6 +73,18 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
     }
   }
+  uint32_t tick = A.tick0;
+  float eps = A.eps;
+  uint32_t slot = 0;
+  if (MODE == MODE_TICK) {
+    tick = A.ctrl->tick;
+    eps = A.ctrl->eps;
+    slot = A.ctrl->write_slot;
+  }
+  const uint32_t genv = (uint32_t)(A.env_offset + d.gid);
+  // the first tick's eps-greedy coin only needs ctrl: drawn while the prologue's loads fly
+  const bool explore0 = (MODE != MODE_STEP && MODE != MODE_Q && eps > 0.0f) &&
+                        u01(philox4x32(tick, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
   if (MODE == MODE_TICK && A.learn) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
@@ -103,14 +115,6 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
   const float* P = Pw;
   SWARM_STAMP(1);
 
-  uint32_t tick = A.tick0;
-  float eps = A.eps;
-  uint32_t slot = 0;
-  if (MODE == MODE_TICK) {
-    tick = A.ctrl->tick;
-    eps = A.ctrl->eps;
-    slot = A.ctrl->write_slot;
-  }
   const int n_ticks = (MODE == MODE_ROLLOUT) ? A.n_ticks : 1;
   float rew_sum[CT], hits_sum = 0.0f;
 #pragma unroll
@@ -146,9 +150,8 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
 
     // ---- eps-greedy (train_gcn_dqn.py:164-167), one Philox coin per env and tick
     const uint32_t tk = tick + (uint32_t)it;
-    const uint32_t genv = (uint32_t)(A.env_offset + d.gid);
-    bool explore = false;
-    if (MODE != MODE_STEP && eps > 0.0f) explore = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
+    bool explore = explore0;
+    if (it > 0 && eps > 0.0f) explore = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
     int action[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {

@@ -5,8 +5,9 @@
 // swarm_adam_step, so the three paths are bit-identical.
 //
 // Reference: train_gcn_dqn.py:125-126 (clip_grad_norm_(model.parameters(), 1);
-// Adam(lr=1e-3)).  torch semantics restated: per-tensor L2 norms, total = norm of
-// norms, coef = max_norm / (total + 1e-6) clamped to 1, grads *= coef; Adam
+// Adam(lr=1e-3)).  torch semantics restated: total = norm of the per-tensor L2 norms
+// (computed here as the global L2 norm, equal up to rounding), coef = max_norm /
+// (total + 1e-6) clamped to 1, grads *= coef; Adam
 // single_tensor: m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g g; denom = sqrt(v)/sqrt(bc2) + eps;
 // w += -(lr/bc1) * m/denom.  bc = 1 - beta^step with beta^step kept as a running
 // double product in the control block (python's beta ** step up to ~1e-16 relative).
@@ -20,13 +21,7 @@ constexpr int kAdamNF4 = N_PARAMS / 4;                 // 418 float4 = floats 0.
 constexpr int kAdamNJ = (kAdamNF4 + kAdamNT - 1) / kAdamNT;
 static_assert(kAdamNF4 * 4 + 1 == N_PARAMS, "one tail element (lin2.bias[8])");
 
-// tensor index of float4 i (every tensor boundary is a multiple of 4 floats)
-__device__ inline int tensor_of_f4(int i) {
-  return i < OFF_ATT_DST / 4 ? 0 : i < OFF_BIAS / 4 ? 1 : i < OFF_W / 4 ? 2 : i < OFF_W1 / 4 ? 3
-       : i < OFF_B1 / 4 ? 4 : i < OFF_W2 / 4 ? 5 : i < OFF_B2 / 4 ? 6 : 7;
-}
-
-// beta^step running products live in the control block (doubles in the pad words)
+// beta^step running products live in the control block (two doubles, words 10-13)
 __device__ inline double ctrl_get_double(const swarm_ctrl* c, int word) {
   const uint32_t* p = &c->beta_pow[word];
   return __hiloint2double((int)p[1], (int)p[0]);
@@ -100,15 +95,15 @@ __device__ inline void adam_elem(float g, float& w, float& m, float& v, float on
 
 // One optimizer step in registers by the whole workgroup (kAdamNT threads; contains
 // __syncthreads).  step_size / inv_bc2_sqrt: ctrl's scalars of this step.  Returns the
-// pre-clip global norm.  red: LDS scratch of >= 8 * (kAdamNT/64) + 8 floats.
+// pre-clip global norm.  red: LDS scratch of >= kAdamNT/64 floats.
 template <int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
 __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float step_size, float inv_bc2_sqrt,
                                    int tid, float* red) {
 #define AD_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
   const float inv_w = 1.0f / (float)hp.world_size;
-  float ss[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ss[k] = 0.0f;
+  // clip_grad_norm_: the norm of the per-tensor norms == the global L2 norm up to rounding
+  // (<= ~1e-7 relative on the clip coefficient); one fixed-order reduction
+  float ss = 0.0f;
 #pragma unroll
   for (int j = 0; j < kAdamNJ; ++j) {
     const int i = tid + kAdamNT * j;
@@ -116,29 +111,20 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float 
     if (hp.world_size > 1) { g.x = g.x * inv_w; g.y = g.y * inv_w; g.z = g.z * inv_w; g.w = g.w * inv_w; }
     R.g[j] = g;
     const float d = ((g.x * g.x + g.y * g.y) + g.z * g.z) + g.w * g.w;
-    const int t = i < kAdamNF4 ? tensor_of_f4(i) : -1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ss[k] = ss[k] + (t == k ? d : 0.0f);
+    ss = ss + (i < kAdamNF4 ? d : 0.0f);
   }
   if (hp.world_size > 1) R.gt = R.gt * inv_w;
-  if (tid == 0) ss[7] = ss[7] + R.gt * R.gt;
+  if (tid == 0) ss = ss + R.gt * R.gt;
   AD_STAMP(0);
   constexpr int NW = kAdamNT / 64;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float s = wave_sum(ss[k]);
-    if ((tid & 63) == 0) red[k * NW + (tid >> 6)] = s;
+  {
+    const float s = wave_sum(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
   }
   __syncthreads();
-  float nn = 0.0f;
+  float nn = red[0];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float s = red[k * NW];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) s = s + red[k * NW + w];
-    const float nk = sqrtf(s);
-    nn = nn + nk * nk;
-  }
+  for (int w = 1; w < NW; ++w) nn = nn + red[w];
   const float total_norm = sqrtf(nn);
   AD_STAMP(1);
   const float coef = hp.max_norm / (total_norm + 1e-6f);
