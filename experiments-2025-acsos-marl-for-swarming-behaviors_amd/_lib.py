@@ -52,7 +52,7 @@ class SwarmLearner(ctypes.Structure):
 
 
 # swarm_ctrl is 16 x 4-byte words on the device; field -> word index
-CTRL_WORDS = 16
+CTRL_WORDS = 32
 CTRL = dict(tick=0, write_slot=1, filled_slots=2, adam_step=3, eps=4, loss=5, grad_norm=6, trained=7, episode=8,
             adam_step_size=14, adam_inv_bc2=15)
 
@@ -68,9 +68,9 @@ _PROTOS = {
     "swarm_act_step": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, POINTER(SwarmReplay), c_void_p,
                                  POINTER(SwarmActOut), c_void_p]),
     "swarm_train_act_step": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
-                                       POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p]),
+                                       POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p, c_void_p]),
     "swarm_reduce_advance": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p, POINTER(SwarmLearner),
-                                       c_int32, c_void_p, c_void_p, c_void_p]),
+                                       c_int32, c_void_p, c_void_p]),
     "swarm_sample_prepare": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_int32, c_void_p, c_void_p,
                                        c_void_p]),
     "swarm_adam_flush": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,

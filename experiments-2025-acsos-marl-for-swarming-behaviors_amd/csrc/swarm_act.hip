@@ -33,6 +33,7 @@ struct ActArgs {
   swarm_learner lr;
   swarm_adam_cfg hp;
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
+  int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
 };
 
 constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
@@ -73,13 +74,17 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
     }
   }
+  // the whole control block in registers, loaded once and up front (two scalar lines in
+  // flight together instead of dependent loads behind branches)
+  swarm_ctrl cc = {};
+  if (MODE == MODE_TICK) cc = *A.ctrl;
   uint32_t tick = A.tick0;
   float eps = A.eps;
   uint32_t slot = 0;
   if (MODE == MODE_TICK) {
-    tick = A.ctrl->tick;
-    eps = A.ctrl->eps;
-    slot = A.ctrl->write_slot;
+    tick = cc.tick;
+    eps = cc.eps;
+    slot = cc.write_slot;
   }
   const uint32_t genv = (uint32_t)(A.env_offset + d.gid);
   // the first tick's eps-greedy coin only needs ctrl: drawn while the prologue's loads fly
@@ -91,9 +96,9 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
     const int tid = threadIdx.x;
     AdamRegs R;
     R.load(A.lr.grad, A.lr.w_cur, A.lr.m_cur, A.lr.v_cur, tid);
-    const uint32_t pending = A.ctrl->trained;
-    const uint32_t tnow = A.ctrl->tick;
-    const float step_size = A.ctrl->adam_step_size, inv_bc2 = A.ctrl->adam_inv_bc2;
+    const uint32_t pending = cc.trained;
+    const uint32_t tnow = cc.tick;
+    const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;
     float gn = 0.0f;
     SWARM_STAMP(20);
     if (pending) gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, tid, red);
@@ -284,6 +289,20 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       }
     }
   }
+if (MODE == MODE_TICK && A.sample_out) {   // at the end of every wave: nothing waits on it
+    // this tick's TD batch (GraphReplayBuffer.sample, train_gcn_dqn.py:40): the keyed
+    // permutation of swarm_td_grad's in-kernel draw, one index per lane of a wave; the
+    // key comes from ctrl's cache (prepared by the previous reduce launch)
+    const uint32_t cap = (uint32_t)A.replay.capacity;
+    const uint32_t filled = cc.filled_slots;
+    const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)A.B;
+    if (ng >= (uint32_t)A.hp.batch) {
+      const SampleKey sk = sample_key_cached(&cc, ng, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, tick);
+      const int nw = (int)gridDim.x * kActWPB;
+      for (int i = (int)blockIdx.x * kActWPB + w + nw * d.lane; i < A.hp.batch; i += nw * 64)
+        A.sample_out[i] = (int32_t)sample_index((uint32_t)i, sk);
+    }
+  }
   SWARM_STAMP(4);
 }
 
@@ -468,12 +487,13 @@ int swarm_act_step(const swarm_config* cfg, const float* params, float* state, c
 }
 
 int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
-                         const swarm_replay* replay, const swarm_ctrl* ctrl, const swarm_act_out* out, void* stream) {
+                         const swarm_replay* replay, const swarm_ctrl* ctrl, const swarm_act_out* out,
+                         int32_t* sample_out, void* stream) {
   if (int e = check_cfg(cfg)) return e;
   if (!ctrl || !hp || !lr || cfg->graph == SWARM_GRAPH_DENSE || hp->world_size < 1 || hp->update_target_every < 1)
     return SWARM_E_BADARG;
   ActArgs a = make_args(cfg);
-  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp;
+  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = sample_out;
   static const bool no_gn = getenv("SWARM_NO_GN") != nullptr;   // A/B knob (diagnostics)
   a.grad_norm_out = no_gn ? nullptr : const_cast<float*>(&ctrl->grad_norm);
   if (replay) a.replay = *replay;

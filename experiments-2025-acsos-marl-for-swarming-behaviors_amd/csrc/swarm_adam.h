@@ -37,11 +37,17 @@ constexpr int CTRL_B2POW = 2;   // beta_pow[2..3] = beta2^adam_step
 // step_size = lr / bias_correction1, bias_correction2_sqrt = sqrt(bias_correction2), both
 // in double), stored in ctrl as floats by whoever advances the powers, so the optimizer
 // step itself carries no double-precision work.  One function for every path.
+// b1pow / b2pow: beta^s after s steps -> the scalars of step s + 1
+__device__ inline void adam_next_scalars(const swarm_adam_cfg& hp, double b1pow, double b2pow, float& step_size,
+                                         float& inv_bc2) {
+  const double b1n = b1pow * (double)hp.beta1;
+  const double b2n = b2pow * (double)hp.beta2;
+  step_size = (float)((double)hp.lr / (1.0 - b1n));
+  inv_bc2 = 1.0f / (float)sqrt(1.0 - b2n);
+}
 __device__ inline void ctrl_store_next_scalars(swarm_ctrl* c, const swarm_adam_cfg& hp) {
-  const double b1n = ctrl_get_double(c, CTRL_B1POW) * (double)hp.beta1;
-  const double b2n = ctrl_get_double(c, CTRL_B2POW) * (double)hp.beta2;
-  c->adam_step_size = (float)((double)hp.lr / (1.0 - b1n));
-  c->adam_inv_bc2 = 1.0f / (float)sqrt(1.0 - b2n);
+  adam_next_scalars(hp, ctrl_get_double(c, CTRL_B1POW), ctrl_get_double(c, CTRL_B2POW), c->adam_step_size,
+                    c->adam_inv_bc2);
 }
 
 struct AdamRegs {

@@ -113,6 +113,17 @@ __host__ __device__ inline SampleKey sample_key(uint32_t n, uint32_t k0, uint32_
   s.n = n;
   return s;
 }
+// the key of tick `rnd` from ctrl's cache when its tags match, else derived
+__device__ inline SampleKey sample_key_cached(const swarm_ctrl* c, uint32_t n, uint32_t k0, uint32_t k1, uint32_t rnd) {
+  if (c->sample_tick == rnd && c->sample_n == n) {
+    SampleKey s;
+    s.rk[0] = c->sample_key[0]; s.rk[1] = c->sample_key[1]; s.rk[2] = c->sample_key[2]; s.rk[3] = c->sample_key[3];
+    s.bits = (int)c->sample_bits;
+    s.n = n;
+    return s;
+  }
+  return sample_key(n, k0, k1, rnd);
+}
 __host__ __device__ inline uint32_t feistel(uint32_t x, const SampleKey& s) {
   const int lo_bits = s.bits / 2, hi_bits = s.bits - lo_bits;
   const uint32_t lo_mask = (1u << lo_bits) - 1u, hi_mask = (1u << hi_bits) - 1u;

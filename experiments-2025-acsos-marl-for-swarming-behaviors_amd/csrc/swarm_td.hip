@@ -441,8 +441,7 @@ struct ReduceArgs {
   swarm_ctrl* ctrl;
   int capacity, B, N, batch;
   swarm_adam_cfg hp;
-  int32_t* sample_next;   // fused tick: replay indices of the NEXT tick's TD batch
-  uint32_t k0, k1;        // sampling key (seed ^ rank salt)
+  uint32_t k0, k1;        // replay-sampling key (seed ^ rank salt)
 };
 
 // 1024 threads = 64 columns x 16 slab groups; group g sums a contiguous run of at most
@@ -451,9 +450,37 @@ struct ReduceArgs {
 constexpr int kRedGroups = 16;
 __global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs A) {
   __shared__ float part[kRedGroups][64];
+  SWARM_STAMP(28);
   const int c = threadIdx.x & 63;
   const int col = blockIdx.x * 64 + c;
   const int q = threadIdx.x >> 6;
+  // advance mode: the thread owning column N_PARAMS is the control block's single writer.
+  // It reads ctrl and prepares the whole update (incl. the double-precision Adam scalars
+  // of the next step) before the slab loads return, and stores it at the end.
+  const bool writer = A.advance && col == N_PARAMS && q == 0;
+  swarm_ctrl* C = A.ctrl;
+  uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
+  double b1p = 1.0, b2p = 1.0;
+  float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
+  if (writer) {
+    c_trained = C->trained; c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
+    b1p = ctrl_get_double(C, CTRL_B1POW);
+    b2p = ctrl_get_double(C, CTRL_B2POW);
+    if (c_trained) {   // the step this tick's act kernel applied
+      b1p = b1p * (double)A.hp.beta1;
+      b2p = b2p * (double)A.hp.beta2;
+      adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
+    }
+  }
+  // ... and the next tick's replay-sampling key (ctrl's cache for swarm_train_act_step)
+  SampleKey nk = {};
+  uint32_t nk_n = 0;
+  if (writer) {
+    const uint32_t cap = (uint32_t)A.capacity;
+    const uint32_t f1 = c_filled + 1 < cap ? c_filled + 1 : cap;   // filled after this tick
+    nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;           // graphs the next tick samples from
+    nk = sample_key(nk_n, A.k0, A.k1, c_tick + 1);
+  }
   const int per = (A.n_slabs + kRedGroups - 1) / kRedGroups;
   const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
   float s = 0.0f;
@@ -471,48 +498,38 @@ __global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs
     else if (q == 1) A.lr.m_cur[col] = A.lr.m_nxt[col];
     else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
   }
+  SWARM_STAMP(29);
   part[q][c] = s;
-  // the block holding column N_PARAMS also owns the control block: it reads ctrl
-  // before its single writer updates it, and draws the next tick's sample indices
-  // (the permutation the TD kernel would otherwise compute on its critical path)
-  const bool owner = A.advance && (blockIdx.x == (N_PARAMS / 64));
-  uint32_t c_tick = 0, c_filled = 0;
-  if (owner) { c_tick = A.ctrl->tick; c_filled = A.ctrl->filled_slots; }
   __syncthreads();
-  if (owner && A.sample_next) {
-    const uint32_t cap = (uint32_t)A.capacity;
-    const uint32_t f1 = c_filled + 1 < cap ? c_filled + 1 : cap;           // filled after this tick
-    const uint32_t vs = f1 + 1 < cap ? f1 + 1 : cap;                        // valid slots next tick
-    const uint32_t ng = vs * (uint32_t)A.B;
-    if (ng >= (uint32_t)A.batch) {
-      const SampleKey sk = sample_key(ng, A.k0, A.k1, c_tick + 1);
-      for (int i = threadIdx.x; i < A.batch; i += blockDim.x) A.sample_next[i] = (int32_t)sample_index((uint32_t)i, sk);
-    }
-  }
+  SWARM_STAMP(30);
   if (q == 0 && col <= N_PARAMS) {
     float tot = part[0][c];
 #pragma unroll
     for (int gi = 1; gi < kRedGroups; ++gi) tot = tot + part[gi][c];
     A.grad[col] = tot;
-    if (A.advance && col == N_PARAMS) {   // one thread: record the pending update, advance the tick
-      swarm_ctrl* C = A.ctrl;
+    if (writer) {   // record the pending update, advance the tick
       const uint32_t cap = (uint32_t)A.capacity;
-      const uint32_t filled = C->filled_slots;
-      const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
+      const uint32_t valid_slots = c_filled + 1 < cap ? c_filled + 1 : cap;
       const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
-      if (C->trained) {                                   // applied by this tick's act kernel
-        C->adam_step = C->adam_step + 1;
-        ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * (double)A.hp.beta1);
-        ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * (double)A.hp.beta2);
-        ctrl_store_next_scalars(C, A.hp);
+      if (c_trained) {
+        C->adam_step = c_step + 1;
+        ctrl_set_double(C, CTRL_B1POW, b1p);
+        ctrl_set_double(C, CTRL_B2POW, b2p);
+        C->adam_step_size = next_step_size;
+        C->adam_inv_bc2 = next_inv_bc2;
       }
       C->trained = trained;
       C->loss = trained ? tot / (float)((size_t)A.batch * A.N) : 0.0f;
-      C->tick = C->tick + 1;
-      C->write_slot = (C->write_slot + 1) % cap;
+      C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
+      C->sample_bits = (uint32_t)nk.bits;
+      C->sample_n = nk_n;
+      C->sample_tick = c_tick + 1;
+      C->tick = c_tick + 1;
+      C->write_slot = (c_slot + 1) % cap;
       C->filled_slots = valid_slots;
     }
   }
+  SWARM_STAMP(31);
 }
 
 // ---------------------------------------------------------------- clip + Adam + target sync
@@ -580,6 +597,7 @@ __global__ void ctrl_init_kernel(swarm_adam_cfg hp, float eps, swarm_ctrl* C) {
   uint32_t* w = reinterpret_cast<uint32_t*>(C);
   for (int i = 0; i < (int)(sizeof(swarm_ctrl) / 4); ++i) w[i] = 0u;
   C->eps = eps;
+  C->sample_tick = 0xFFFFFFFFu;   // empty sampling-key cache
   ctrl_set_double(C, CTRL_B1POW, 1.0);
   ctrl_set_double(C, CTRL_B2POW, 1.0);
   ctrl_store_next_scalars(C, hp);
@@ -657,7 +675,7 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
 }
 
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
-                         int32_t replay_capacity, swarm_ctrl* ctrl, int32_t* sample_next, void* stream) {
+                         int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
   if (int e = check_td(cfg, hp)) return e;
   if (!lr || !ctrl || replay_capacity < 1) return SWARM_E_BADARG;
   ReduceArgs a = {};
@@ -665,7 +683,6 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
   a.hp = *hp;
-  a.sample_next = sample_next;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
   hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(64 * kRedGroups), 0, (hipStream_t)stream, a);

@@ -4,8 +4,9 @@ all resident in HBM, driven through libswarm_hip.so.
 One fused training tick (the reference's hot loop, src/training/train_gcn_dqn.py:153-178):
 
     swarm_train_act_step  [clip + Adam of the previous tick's gradient, target sync]
-                          graph -> GAT Q -> eps-greedy -> env.step -> replay push     (1 launch)
-    swarm_td_grad         sample -> target fwd -> online fwd -> TD loss -> backward    (1 launch)
+                          graph -> GAT Q -> eps-greedy -> env.step -> replay push,
+                          this tick's TD batch indices                                (1 launch)
+    swarm_td_grad         batch rows -> target fwd -> online fwd -> TD loss -> backward (1 launch)
     swarm_reduce_advance  deterministic slab sum, ping-pong copy-back, ctrl advance    (1 launch)
     [all_reduce(grad) over RCCL when world_size > 1]
 
@@ -139,7 +140,6 @@ class SwarmEngine:
         self.grad = torch.zeros(N_PARAMS + 3, **f32)
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
-        self._samples_valid = False   # fused path: indices for the next TD batch are ready
         # per-tick outputs
         self.q = torch.zeros(n_envs, n_agents, 9, **f32)
         self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
@@ -152,10 +152,6 @@ class SwarmEngine:
         self.out_min = SwarmActOut(0, 0, ptr(self.reward), 0, ptr(self.avg_dist), ptr(self.hits), 0, 0, 0, 0)
 
     # ------------------------------------------------------------------ control block
-    def invalidate(self):
-        """Call after editing ctrl / the replay by hand: the fused tick re-draws its samples."""
-        self._samples_valid = False
-
     def set_eps(self, eps: float):
         self.ctrl.view(torch.float32)[CTRL["eps"]].fill_(float(eps))
 
@@ -183,14 +179,12 @@ class SwarmEngine:
 
     # ------------------------------------------------------------------ acting
     def act(self, push: bool = True, full_out: bool = True):
-        self._samples_valid = False
         check(self.lib.swarm_act_step(ctypes_ref(self.cfg), ptr(self.params), ptr(self.state),
                                       ctypes_ref(self.replay) if push else None, ptr(self.ctrl),
                                       ctypes_ref(self.out if full_out else self.out_min), stream_ptr()),
               "swarm_act_step")
 
     def advance(self):
-        self._samples_valid = False
         check(self.lib.swarm_ctrl_advance(ctypes_ref(self.cfg), ctypes_ref(self.replay), ptr(self.ctrl),
                                           stream_ptr()), "swarm_ctrl_advance")
 
@@ -234,7 +228,6 @@ class SwarmEngine:
 
     def td_update(self, sample_in=None, sample_out=None):
         """Unfused TD update (API path): applies the optimizer step immediately."""
-        self._samples_valid = False
         self.flush()
         self.td_grad(sample_in, sample_out)
         self.allreduce_grad()
@@ -248,7 +241,8 @@ class SwarmEngine:
     def launch_train_act(self):
         check(self.lib.swarm_train_act_step(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
                                             ptr(self.state), ctypes_ref(self.replay), ptr(self.ctrl),
-                                            ctypes_ref(self.out_min), stream_ptr()), "swarm_train_act_step")
+                                            ctypes_ref(self.out_min), ptr(self.samples), stream_ptr()),
+              "swarm_train_act_step")
 
     def launch_td(self):
         check(self.lib.swarm_td_grad(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.w_nxt), ptr(self.target),
@@ -260,21 +254,18 @@ class SwarmEngine:
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
     def train_tick(self, full_out: bool = False):
-        """Fused training tick: 3 launches (+ an RCCL all-reduce when world_size > 1)."""
+        """Fused training tick: 3 launches (+ an RCCL all-reduce when world_size > 1).
+        The act launch also draws this tick's TD batch indices (self.samples)."""
         cfg, hp = ctypes_ref(self.cfg), ctypes_ref(self.hp)
-        if not self._samples_valid:
-            check(self.lib.swarm_sample_prepare(cfg, hp, self.capacity, ptr(self.ctrl), ptr(self.samples),
-                                                stream_ptr()), "swarm_sample_prepare")
         check(self.lib.swarm_train_act_step(cfg, hp, ctypes_ref(self.learner), ptr(self.state),
                                             ctypes_ref(self.replay), ptr(self.ctrl),
-                                            ctypes_ref(self.out if full_out else self.out_min), stream_ptr()),
-              "swarm_train_act_step")
+                                            ctypes_ref(self.out if full_out else self.out_min), ptr(self.samples),
+                                            stream_ptr()), "swarm_train_act_step")
         check(self.lib.swarm_td_grad(cfg, hp, ptr(self.w_nxt), ptr(self.target), ctypes_ref(self.replay),
                                      ptr(self.ctrl), ptr(self.samples), None, ptr(self.slabs), stream_ptr()),
               "swarm_td_grad")
         check(self.lib.swarm_reduce_advance(cfg, hp, ptr(self.slabs), ctypes_ref(self.learner), self.capacity,
-                                            ptr(self.ctrl), ptr(self.samples), stream_ptr()), "swarm_reduce_advance")
-        self._samples_valid = True
+                                            ptr(self.ctrl), stream_ptr()), "swarm_reduce_advance")
         self.allreduce_grad()
 
     # ------------------------------------------------------------------ hipGraph

@@ -67,7 +67,12 @@ typedef struct swarm_ctrl {
                              (words 10-13)                                                  */
   float adam_step_size;   /* Adam scalars of optimizer step adam_step + 1, kept current by the */
   float adam_inv_bc2;     /* library: lr / (1 - beta1^(s+1)) and 1 / sqrt(1 - beta2^(s+1))     */
-} swarm_ctrl;
+  uint32_t sample_key[4]; /* cache: replay-sampling round keys of tick `sample_tick` over      */
+  uint32_t sample_tick;   /* `sample_n` graphs, prepared by swarm_reduce_advance (words 16-22); */
+  uint32_t sample_n;      /* recomputed from (tick, n) whenever the tags do not match          */
+  uint32_t sample_bits;
+  uint32_t pad1[9];
+} swarm_ctrl;           /* 32 words */
 /* A fresh control block comes from swarm_ctrl_init (all counters 0, beta powers 1). */
 
 /* Replay ring (GraphReplayBuffer, train_gcn_dqn.py:25-48), SoA, per rank:
@@ -163,20 +168,19 @@ int swarm_act_step(const swarm_config* cfg, const float* params, float* state,
 /* Fused training tick, acting half (train_gcn_dqn.py:161-172 + the optimizer step
  * of the previous tick's TD loss, :125-133): if ctrl->trained, apply
  * clip_grad_norm_ + Adam to (w_cur, grad) in every block (LDS image), block 0
- * persists w_nxt/m_nxt/v_nxt (+ target sync); then act with w_nxt.
+ * persists w_nxt/m_nxt/v_nxt (+ target sync); then act with w_nxt.  If sample_out
+ * != NULL it also draws this tick's TD batch indices [hp->batch] (exactly what
+ * swarm_td_grad would draw in-kernel; pass them to it as sample_in).
  * Sequence per tick: swarm_train_act_step -> swarm_td_grad(params = w_nxt) ->
  * swarm_reduce_advance [-> all-reduce(grad)]. */
 int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr,
                          float* state, const swarm_replay* replay, const swarm_ctrl* ctrl,
-                         const swarm_act_out* out, void* stream);
+                         const swarm_act_out* out, int32_t* sample_out, void* stream);
 
 /* Slab sum -> lr->grad, copy *_nxt -> *_cur, record the pending update and
- * advance ctrl (tick, replay slot).  If sample_next != NULL it also draws the
- * replay indices [batch] of the next tick's TD batch (pass them to swarm_td_grad
- * as sample_in: identical to the in-kernel draw, off the TD critical path). */
+ * advance ctrl (tick, replay slot, the next step's Adam scalars). */
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
-                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
-                         int32_t* sample_next, void* stream);
+                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
 
 /* Draw the TD batch's replay indices [batch] for the tick ctrl describes
  * (GraphReplayBuffer.sample, train_gcn_dqn.py:40: keyed permutation, distinct ids). */
