@@ -106,7 +106,7 @@ def load(require_gpu: bool = True):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.swarm_abi_version() != 1:
+        if lib.swarm_abi_version() != 2:
             raise RuntimeError("libswarm_hip ABI mismatch")
         _lib = lib
     return _lib

@@ -444,16 +444,18 @@ struct ReduceArgs {
   uint32_t k0, k1;        // replay-sampling key (seed ^ rank salt)
 };
 
-// 1024 threads = 64 columns x 16 slab groups; group g sums a contiguous run of at most
-// 16 slabs with every load issued before the ordered adds, then the 16 group sums are
+// 1024 threads = 16 columns x 64 slab groups (105 blocks: the 1.7 MB of freshly written
+// slabs is read by many CUs at once, 16 KB each); group g sums a contiguous run of slabs
+// with every load issued before the ordered adds, then the 64 group sums of a column are
 // added in group order (fixed order -> bitwise reproducible run to run).
-constexpr int kRedGroups = 16;
-__global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs A) {
-  __shared__ float part[kRedGroups][64];
+constexpr int kRedCols = 16;
+constexpr int kRedGroups = 64;
+__global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(ReduceArgs A) {
+  __shared__ float part[kRedGroups][kRedCols];
   SWARM_STAMP(28);
-  const int c = threadIdx.x & 63;
-  const int col = blockIdx.x * 64 + c;
-  const int q = threadIdx.x >> 6;
+  const int c = threadIdx.x % kRedCols;
+  const int col = blockIdx.x * kRedCols + c;
+  const int q = threadIdx.x / kRedCols;
   // advance mode: the thread owning column N_PARAMS is the control block's single writer.
   // It reads ctrl and prepares the whole update (incl. the double-precision Adam scalars
   // of the next step) before the slab loads return, and stores it at the end.
@@ -485,12 +487,12 @@ __global__ __launch_bounds__(64 * kRedGroups) void grad_reduce_kernel(ReduceArgs
   const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
   float s = 0.0f;
   if (col <= N_PARAMS) {
-    for (int b = b0; b < b1; b += 16) {
-      float v[16];
+    for (int b = b0; b < b1; b += 8) {
+      float v[8];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = (b + j < b1) ? A.slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
+      for (int j = 0; j < 8; ++j) v[j] = (b + j < b1) ? A.slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s = s + v[j];
+      for (int j = 0; j < 8; ++j) s = s + v[j];
     }
   }
   if (A.advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
@@ -670,7 +672,8 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
   if (int e = check_td(cfg, hp)) return e;
   ReduceArgs a = {};
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = grad;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(64 * kRedGroups), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + kRedCols - 1) / kRedCols), dim3(kRedCols * kRedGroups), 0,
+                     (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
@@ -685,7 +688,8 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.hp = *hp;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + 63) / 64), dim3(64 * kRedGroups), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + kRedCols - 1) / kRedCols), dim3(kRedCols * kRedGroups), 0,
+                     (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 1
+#define SWARM_ABI_VERSION 2
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */

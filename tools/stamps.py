@@ -73,12 +73,13 @@ def main():
     report(td[:, :gpb].reshape(-1), TD, blocks * gpb, TD_ORDER)
     print("td_kernel target waves:")
     report(td[:, gpb:2 * gpb].reshape(-1), TD, blocks * gpb, TD_ORDER)
-    red = st.cpu().numpy()[: 27 * 16 * 32].reshape(27, 16, 32)
+    nrb, own = (1674 + 15) // 16, 1673 // 16          # grad_reduce blocks (16 columns each), owner block
+    red = st.cpu().numpy()[: nrb * 16 * 32].reshape(nrb, 16, 32)
     RED = {28: "entry", 29: "slab loads + partial sums", 30: "LDS combine + barrier", 31: "final sum, copy-back, ctrl/samples"}
     print("grad_reduce_kernel (advance), ordinary blocks:")
-    report(red[:26].reshape(-1), RED, 26 * 16, [28, 29, 30, 31])
+    report(red[:own].reshape(-1), RED, own * 16, [28, 29, 30, 31])
     print("grad_reduce_kernel owner block (ctrl + next-tick samples):")
-    report(red[26:27].reshape(-1), RED, 16, [28, 29, 30, 31])
+    report(red[own:own + 1].reshape(-1), RED, 16, [28, 29, 30, 31])
 
 
 if __name__ == "__main__":
