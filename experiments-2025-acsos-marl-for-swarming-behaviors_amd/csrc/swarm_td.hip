@@ -460,10 +460,23 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
   // It reads ctrl and prepares the whole update (incl. the double-precision Adam scalars
   // of the next step) before the slab loads return, and stores it at the end.
   const bool writer = A.advance && col == N_PARAMS && q == 0;
+  const int per = (A.n_slabs + kRedGroups - 1) / kRedGroups;
+  const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
+  // first chunk of this thread's slab column in flight before anything else
+  constexpr int kChunk = 8;
+  float v0[kChunk];
+#pragma unroll
+  for (int j = 0; j < kChunk; ++j)
+    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? A.slabs[(size_t)(b0 + j) * (N_PARAMS + 1) + col] : 0.0f;
+  // advance mode: the thread owning column N_PARAMS is the control block's single writer.
+  // It prepares the whole update (incl. the double-precision Adam scalars of the next
+  // step and the next tick's sampling key) while the slab loads fly, stores it at the end.
   swarm_ctrl* C = A.ctrl;
   uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
   double b1p = 1.0, b2p = 1.0;
   float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
+  SampleKey nk = {};
+  uint32_t nk_n = 0, nk_tick = 0;
   if (writer) {
     c_trained = C->trained; c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
     b1p = ctrl_get_double(C, CTRL_B1POW);
@@ -474,25 +487,26 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
       adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
     }
   }
-  // ... and the next tick's replay-sampling key (ctrl's cache for swarm_train_act_step)
-  SampleKey nk = {};
-  uint32_t nk_n = 0;
-  if (writer) {
+  // a second wave of the same block prepares the next tick's sampling key in parallel
+  const bool key_writer = A.advance && col == N_PARAMS && q == 4;
+  if (key_writer) {
     const uint32_t cap = (uint32_t)A.capacity;
-    const uint32_t f1 = c_filled + 1 < cap ? c_filled + 1 : cap;   // filled after this tick
-    nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;           // graphs the next tick samples from
-    nk = sample_key(nk_n, A.k0, A.k1, c_tick + 1);
+    const uint32_t filled = C->filled_slots;
+    const uint32_t f1 = filled + 1 < cap ? filled + 1 : cap;   // filled after this tick
+    nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;       // graphs the next tick samples from
+    nk_tick = C->tick + 1;
+    nk = sample_key(nk_n, A.k0, A.k1, nk_tick);
   }
-  const int per = (A.n_slabs + kRedGroups - 1) / kRedGroups;
-  const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
-  float s = 0.0f;
+  float s = v0[0];
+#pragma unroll
+  for (int j = 1; j < kChunk; ++j) s = s + v0[j];
   if (col <= N_PARAMS) {
-    for (int b = b0; b < b1; b += 8) {
-      float v[8];
+    for (int b = b0 + kChunk; b < b1; b += kChunk) {
+      float v[kChunk];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (b + j < b1) ? A.slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
+      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? A.slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s = s + v[j];
+      for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }
   }
   if (A.advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
@@ -522,14 +536,16 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
       }
       C->trained = trained;
       C->loss = trained ? tot / (float)((size_t)A.batch * A.N) : 0.0f;
-      C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
-      C->sample_bits = (uint32_t)nk.bits;
-      C->sample_n = nk_n;
-      C->sample_tick = c_tick + 1;
       C->tick = c_tick + 1;
       C->write_slot = (c_slot + 1) % cap;
       C->filled_slots = valid_slots;
     }
+  }
+  if (key_writer) {   // after the barrier: every thread of the block has read ctrl
+    C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
+    C->sample_bits = (uint32_t)nk.bits;
+    C->sample_n = nk_n;
+    C->sample_tick = nk_tick;
   }
   SWARM_STAMP(31);
 }
