@@ -12,8 +12,11 @@ SOURCES = ["swarm_act.hip", "swarm_td.hip"]
 HEADERS = ["swarm_common.h", "swarm_knn.h", "swarm_wpg.h", "swarm_dl.h", "swarm_env.h", "swarm_adam.h"]
 OUT = os.path.join(HERE, "libswarm_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# kernarg preload: the leading 14 kernel-argument dwords arrive in SGPRs at wave start (the
+# kernels put their first round trip's pointers there); older firmware runs the emitted
+# compatibility prologue that loads them instead.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-         "-Wall", "-Wno-unused-function"]
+         "-Wall", "-Wno-unused-function", "-mllvm", "-amdgpu-kernarg-preload-count=14"]
 
 
 def _deps():

@@ -41,16 +41,23 @@ constexpr int kActWPB = 4;   // waves (= environments) per act block; the block 
 // One wave per environment in the D layout (swarm_dl.h): lane (c, p) serves agent
 // n = 16 ct + c with row group p.  Block-wide work is only the weight image (LDS),
 // staged from global memory or produced by the fused Adam prologue.
-template <int NS, int MODE>
-__global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
+//
+// The first memory round trip's pointers and the geometry lead the parameter list so that
+// they arrive preloaded in SGPRs (kernarg preload, -amdgpu-kernarg-preload-count): the
+// prologue's loads issue at wave start instead of behind a kernarg-segment fetch.
+template <int NS, int MODE, int SCEN>   // SCEN: compile-time scenario (no speculated OA physics)
+__global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
+                                                          const float* grad, const float* w_cur,
+                                                          const float* m_cur, const float* v_cur, int B, int N,
+                                                          ActArgs A) {
   constexpr int CT = DGeom<NS>::CT;
   __shared__ WScratch<NS> SW[kActWPB];
   __shared__ __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
   __shared__ float red[8 * kActWPB + 8];
+  SWARM_RTSTAMP(30);
   SWARM_STAMP(0);
   const int w = threadIdx.x >> 6;
-  const int N = A.N;
-  const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * kActWPB + w, A.B);
+  const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * kActWPB + w, B);
   const WView<NS> V = SW[w].view();
   WSmall<NS>& sm = SW[w].sm;
   const int c = d.c, p = d.p;
@@ -70,14 +77,14 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       F.x[ct][0] = valid[ct] ? A.x[node[ct] * kFeat + p] : 0.0f;
       F.x[ct][1] = (valid[ct] && 4 + p < kFeat) ? A.x[node[ct] * kFeat + 4 + p] : 0.0f;
     } else {
-      const float4 st = *reinterpret_cast<const float4*>(A.state + node[ct] * 4);
+      const float4 st = *reinterpret_cast<const float4*>(state + node[ct] * 4);
       if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
     }
   }
   // the whole control block in registers, loaded once and up front (two scalar lines in
   // flight together instead of dependent loads behind branches)
   swarm_ctrl cc = {};
-  if (MODE == MODE_TICK) cc = *A.ctrl;
+  if (MODE == MODE_TICK) cc = *ctrl;
   uint32_t tick = A.tick0;
   float eps = A.eps;
   uint32_t slot = 0;
@@ -90,12 +97,25 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
   // the first tick's eps-greedy coin only needs ctrl: drawn while the prologue's loads fly
   const bool explore0 = (MODE != MODE_STEP && MODE != MODE_Q && eps > 0.0f) &&
                         u01(philox4x32(tick, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
+  // the late stores' pointers fetched from the kernarg segment now, beside the wait
+  // explore0 already has, and pinned in SGPRs: no kernarg round trip later in the wave
+  float* rp_s = A.replay.s;
+  float* rp_sn = A.replay.s_next;
+  float* rp_r = A.replay.r;
+  uint8_t* rp_a = A.replay.a;
+  float* o_rew = A.out.reward;
+  float* o_avg = A.out.avg_dist;
+  float* o_hits = A.out.hits;
+  int32_t* smp = A.sample_out;
+#if SWARM_PIN
+  asm volatile("" : "+s"(rp_s), "+s"(rp_sn), "+s"(rp_r), "+s"(rp_a), "+s"(o_rew), "+s"(o_avg), "+s"(o_hits), "+s"(smp));
+#endif
   if (MODE == MODE_TICK && A.learn) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
     const int tid = threadIdx.x;
     AdamRegs R;
-    R.load(A.lr.grad, A.lr.w_cur, A.lr.m_cur, A.lr.v_cur, tid);
+    R.load(grad, w_cur, m_cur, v_cur, tid);
     const uint32_t pending = cc.trained;
     const uint32_t tnow = cc.tick;
     const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;
@@ -170,6 +190,7 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       }
     }
 
+    if (it == 0) SWARM_STAMP(5);
     // ---- env.step (VMAS World.step + scenario reward).  The 4 row groups of an agent
     //      split its partner pairs (group p: partners p, p + 4, ...), then every lane sums
     //      the forces in VMAS order: 0 + u, obstacle pair, agent pairs in ascending partner
@@ -186,25 +207,27 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
         *reinterpret_cast<float2*>(fb + 2 * (n * NS + u)) = make_float2(gx, gy);
       }
     }
+    if (it == 0) SWARM_STAMP(6);
     wave_lds_sync();
+    if (it == 0) SWARM_STAMP(7);
     StepOut o[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = min(16 * ct + c, NS - 1);
       float fx = 0.0f + action_level(action[ct] / 3);
       float fy = 0.0f + action_level(action[ct] % 3);
-      if (A.scenario == SWARM_OBSTACLE_AVOIDANCE) {
+      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {
         float gx, gy;
         pair_force(px[ct] - kObstX, py[ct] - kObstY, gx, gy);
         fx = fx + gx; fy = fy + gy;
       }
+      // every slot read at once, no per-partner branch: slots u >= N hold +0 and fx, fy
+      // (started from +0 or +-1) never become -0, so adding them is exact
+      float2 f[NS];
 #pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        if (u < N) {
-          const float2 f = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + u));
-          fx = fx + f.x; fy = fy + f.y;
-        }
-      }
+      for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + u));
+#pragma unroll
+      for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
       o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
       if (16 * ct + c < NS && p == 0) { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }
     }
@@ -218,18 +241,19 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
     for (int j = 1; j < NS; ++j)
       if (j < N) { dsum = dsum + dj[j]; hsum = hsum + hj[j]; }
     float rg = 0.0f;
-    if (A.scenario == SWARM_GOTO) {
+    if (SCEN == SWARM_GOTO) {
       rg = -dj[0];
 #pragma unroll
       for (int j = 1; j < NS; ++j)
         if (j < N) rg = rg + (-dj[j]);   // go_to_position_scenario.py:112-113
     }
+    if (it == 0) SWARM_STAMP(13);
     const float avg = dsum / (float)N;
-    if (A.scenario == SWARM_GOTO) hsum = 0.0f;
+    if (SCEN == SWARM_GOTO) hsum = 0.0f;
 
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const float rew = (A.scenario == SWARM_GOTO) ? rg : oa_reward(o[ct].dgoal, o[ct].dobs);
+      const float rew = (SCEN == SWARM_GOTO) ? rg : oa_reward(o[ct].dgoal, o[ct].dobs);
       const int n = 16 * ct + c;
       if (valid[ct]) {   // the node's four row groups share its stores
         if (MODE == MODE_TICK || MODE == MODE_STEP) {
@@ -240,16 +264,16 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
               A.out.mult[((size_t)d.gid * N + u) * N + n] = (uint8_t)in_mult<NS>(u, n, N, A.graph, sm, nullptr, d.gid);
           if (p == 0) {
             if (A.out.actions) A.out.actions[node[ct]] = action[ct];
-            if (A.out.reward) A.out.reward[node[ct]] = rew;
+            if (o_rew) o_rew[node[ct]] = rew;
             if (n == 0) {
-              if (A.out.avg_dist) A.out.avg_dist[d.gid] = avg;
-              if (A.out.hits) A.out.hits[d.gid] = hsum;
+              if (o_avg) o_avg[d.gid] = avg;
+              if (o_hits) o_hits[d.gid] = hsum;
             }
-          } else if (MODE == MODE_TICK && A.replay.s) {
-            const size_t ri = ((size_t)slot * A.B + d.gid) * N + n;
-            if (p == 1) reinterpret_cast<float4*>(A.replay.s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
-            else if (p == 2) reinterpret_cast<float4*>(A.replay.s_next)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
-            else { A.replay.r[ri] = rew; A.replay.a[ri] = (uint8_t)action[ct]; }
+          } else if (MODE == MODE_TICK && rp_s) {
+            const size_t ri = ((size_t)slot * B + d.gid) * N + n;
+            if (p == 1) reinterpret_cast<float4*>(rp_s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+            else if (p == 2) reinterpret_cast<float4*>(rp_sn)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
+            else { rp_r[ri] = rew; rp_a[ri] = (uint8_t)action[ct]; }
           }
           if (p == 3 && A.out.obs) {
             float* ob = A.out.obs + node[ct] * 6;
@@ -257,12 +281,12 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
           }
         } else if (p == 0) {  // MODE_ROLLOUT
           if (A.out.traj_pos) {
-            const size_t ti = ((size_t)it * A.B + d.gid) * N + n;
+            const size_t ti = ((size_t)it * B + d.gid) * N + n;
             reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o[ct].px, o[ct].py);
           }
           if (n == 0) {
-            if (A.out.traj_dist) A.out.traj_dist[(size_t)it * A.B + d.gid] = avg;
-            if (A.out.traj_hits) A.out.traj_hits[(size_t)it * A.B + d.gid] = hsum;
+            if (A.out.traj_dist) A.out.traj_dist[(size_t)it * B + d.gid] = avg;
+            if (A.out.traj_hits) A.out.traj_hits[(size_t)it * B + d.gid] = hsum;
           }
         }
       }
@@ -270,6 +294,7 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       px[ct] = o[ct].px; py[ct] = o[ct].py; vx[ct] = o[ct].vx; vy[ct] = o[ct].vy;
     }
     hits_sum = hits_sum + hsum;
+    if (it == 0) SWARM_STAMP(14);
     if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && c == 0 && p == 0 && d.live) {
       if (A.out.avg_dist) A.out.avg_dist[d.gid] = avg;
       if (A.out.hits) A.out.hits[d.gid] = hits_sum;
@@ -279,7 +304,7 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     if (valid[ct] && p == 0) {
-      reinterpret_cast<float4*>(A.state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+      reinterpret_cast<float4*>(state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
       if (MODE == MODE_ROLLOUT) {
         if (A.out.reward) A.out.reward[node[ct]] = rew_sum[ct];
         if (A.out.obs) {
@@ -289,21 +314,22 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(ActArgs A) {
       }
     }
   }
-if (MODE == MODE_TICK && A.sample_out) {   // at the end of every wave: nothing waits on it
+if (MODE == MODE_TICK && smp) {   // at the end of every wave: nothing waits on it
     // this tick's TD batch (GraphReplayBuffer.sample, train_gcn_dqn.py:40): the keyed
     // permutation of swarm_td_grad's in-kernel draw, one index per lane of a wave; the
     // key comes from ctrl's cache (prepared by the previous reduce launch)
     const uint32_t cap = (uint32_t)A.replay.capacity;
     const uint32_t filled = cc.filled_slots;
-    const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)A.B;
+    const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)B;
     if (ng >= (uint32_t)A.hp.batch) {
       const SampleKey sk = sample_key_cached(&cc, ng, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, tick);
       const int nw = (int)gridDim.x * kActWPB;
       for (int i = (int)blockIdx.x * kActWPB + w + nw * d.lane; i < A.hp.batch; i += nw * 64)
-        A.sample_out[i] = (int32_t)sample_index((uint32_t)i, sk);
+        smp[i] = (int32_t)sample_index((uint32_t)i, sk);
     }
   }
   SWARM_STAMP(4);
+  SWARM_RTSTAMP(31);
 }
 
 // ---------------------------------------------------------------- reset
@@ -404,9 +430,15 @@ template <int MODE>
 int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   if (tiles == 0) return 0;
   const dim3 grid((tiles + kActWPB - 1) / kActWPB), block(64 * kActWPB);
-  if (a.N <= 8) hipLaunchKernelGGL((act_kernel<8, MODE>), grid, block, 0, st, a);
-  else if (a.N <= 16) hipLaunchKernelGGL((act_kernel<16, MODE>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((act_kernel<32, MODE>), grid, block, 0, st, a);
+  const float *g = a.lr.grad, *w = a.lr.w_cur, *m = a.lr.m_cur, *v = a.lr.v_cur;
+#define SWARM_ACT_LAUNCH(NS, SC) \
+  hipLaunchKernelGGL((act_kernel<NS, MODE, SC>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
+  constexpr int OA = (MODE == MODE_Q) ? SWARM_GOTO : SWARM_OBSTACLE_AVOIDANCE;   // MODE_Q has no physics
+  const bool oa = MODE != MODE_Q && a.scenario == SWARM_OBSTACLE_AVOIDANCE;
+  if (a.N <= 8) { if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO); }
+  else if (a.N <= 16) { if (oa) SWARM_ACT_LAUNCH(16, OA); else SWARM_ACT_LAUNCH(16, SWARM_GOTO); }
+  else { if (oa) SWARM_ACT_LAUNCH(32, OA); else SWARM_ACT_LAUNCH(32, SWARM_GOTO); }
+#undef SWARM_ACT_LAUNCH
   return (int)hipGetLastError();
 }
 

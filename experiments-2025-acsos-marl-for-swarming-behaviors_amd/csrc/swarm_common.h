@@ -202,7 +202,7 @@ __device__ inline float xor32(float v) { return __shfl_xor(v, 32, 64); }
 #define SWARM_STAMPS 0
 #endif
 #if SWARM_STAMPS
-static __device__ unsigned long long* g_swarm_stamps;
+static __constant__ unsigned long long* g_swarm_stamps;
 #define SWARM_STAMP(k)                                                                        \
   do {                                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                        \
@@ -212,9 +212,22 @@ static __device__ unsigned long long* g_swarm_stamps;
     if (g_swarm_stamps && (threadIdx.x & 63) == 0)                                            \
       g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + (k)] = _t;         \
   } while (0)
+// s_memrealtime: the chip-wide 100 MHz clock, comparable across XCDs (launch spans, gaps)
+#define SWARM_RTSTAMP(k)                                                                      \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long _t;                                                                    \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (g_swarm_stamps && (threadIdx.x & 63) == 0)                                            \
+      g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + (k)] = _t;         \
+  } while (0)
 #else
 #define SWARM_STAMP(k) \
   do {              \
+  } while (0)
+#define SWARM_RTSTAMP(k) \
+  do {                \
   } while (0)
 #endif
 

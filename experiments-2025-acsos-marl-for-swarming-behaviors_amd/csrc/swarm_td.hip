@@ -73,8 +73,12 @@ __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*B
 
 // NS node slots per wave holding NS / GS graphs of GS slots (GS = 8 < NS = 16 packs two
 // N <= 8 graphs into one wave: every MFMA column is a real node, one wave per SIMD).
+// The dependent chain's pointers (batch indices -> replay rows) and the geometry lead the
+// parameter list: preloaded into SGPRs (kernarg preload), the index loads issue at wave start.
 template <int NS, int GS>
-__global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
+__global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(const int32_t* sample_in, const float* rs, const float* rs_next,
+                                                                       const float* rr, const uint8_t* ra, int S, int B, int N,
+                                                                       int capacity, TdArgs A) {
   constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;   // GPB: online (= target) waves per block
   constexpr int GPW = NS / GS;                             // graphs per wave
   constexpr int NT = 128 * GPB;
@@ -84,20 +88,20 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
   const int wave = threadIdx.x >> 6;
   const bool online = wave < GPB;
   const int wi = online ? wave : wave - GPB;
-  const int N = A.N;
   const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * GPB + wi, 1 << 30);   // lane geometry; liveness is per graph
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
   const int lane = d.lane, c = d.c, p = d.p;
   float* gslab = A.slabs + (size_t)blockIdx.x * (N_PARAMS + 1);
+  SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
   // ---- fused tick: this wave's replay indices come from the previous launch, so the
   //      dependent pair (index -> replay rows) is issued first and the weight staging and
   //      ctrl reads overlap it.  Indices are clamped into the ring: a skipped tick reads
   //      valid (unused) rows.
-  const uint32_t cap = (uint32_t)A.replay.capacity;
-  const uint32_t ring_graphs = cap * (uint32_t)A.B;
+  const uint32_t cap = (uint32_t)capacity;
+  const uint32_t ring_graphs = cap * (uint32_t)B;
   int sid[CT];     // batch index of this lane's graph
   bool live[CT], nv[CT];
   int jl[CT];      // local node index inside the graph
@@ -108,38 +112,38 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
     const int gi = (GS < NS) ? n / GS : 0;
     jl[ct] = (GS < NS) ? n % GS : n;
     sid[ct] = blockIdx.x * (kTdRows / GS) + wi * GPW + gi;
-    live[ct] = sid[ct] < A.S && n < NS;
+    live[ct] = sid[ct] < S && n < NS;
     nv[ct] = live[ct] && jl[ct] < N;
     gid[ct] = 0;
-    if (A.sample_in) gid[ct] = min((uint32_t)A.sample_in[min(sid[ct], A.S - 1)], ring_graphs - 1u);
+    if (sample_in) gid[ct] = min((uint32_t)sample_in[min(sid[ct], S - 1)], ring_graphs - 1u);
   }
   ParamStage<NT> pon, ptg;
   pon.load(A.params, threadIdx.x);
   ptg.load(A.target, threadIdx.x);
   const uint32_t filled = A.ctrl->filled_slots;
   const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
-  const uint32_t n_graphs = valid_slots * (uint32_t)A.B;
-  if (!A.sample_in) {   // GraphReplayBuffer.sample: random.sample -> keyed permutation
+  const uint32_t n_graphs = valid_slots * (uint32_t)B;
+  if (!sample_in) {   // GraphReplayBuffer.sample: random.sample -> keyed permutation
     const SampleKey sk = sample_key(n_graphs, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, A.ctrl->tick);
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
-      gid[ct] = n_graphs >= (uint32_t)A.S ? sample_index((uint32_t)min(sid[ct], A.S - 1), sk) : 0u;
+      gid[ct] = n_graphs >= (uint32_t)S ? sample_index((uint32_t)min(sid[ct], S - 1), sk) : 0u;
   }
   float rew[CT];
   int act[CT];
   DFwd<NS> F;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
-    const uint32_t slot = gid[ct] / (uint32_t)A.B, genv = gid[ct] % (uint32_t)A.B;
-    const size_t ri = ((size_t)slot * A.B + genv) * N + min(jl[ct], N - 1);
-    const float4 st = reinterpret_cast<const float4*>(online ? A.replay.s : A.replay.s_next)[ri];
-    rew[ct] = A.replay.r[ri];
-    act[ct] = nv[ct] ? (int)A.replay.a[ri] : 0;
+    const uint32_t slot = gid[ct] / (uint32_t)B, genv = gid[ct] % (uint32_t)B;
+    const size_t ri = ((size_t)slot * B + genv) * N + min(jl[ct], N - 1);
+    const float4 st = reinterpret_cast<const float4*>(online ? rs : rs_next)[ri];
+    rew[ct] = rr[ri];
+    act[ct] = nv[ct] ? (int)ra[ri] : 0;
     node_x(st.x, st.y, st.z, st.w, jl[ct], p, F.x[ct]);
     if (!nv[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
   }
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
-  if (n_graphs < (uint32_t)A.S) {
+  if (n_graphs < (uint32_t)S) {
     for (int q = threadIdx.x; q <= N_PARAMS; q += NT) gslab[q] = 0.0f;
     return;
   }
@@ -427,6 +431,7 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(TdArgs A) {
     }
   }
   SWARM_STAMP(7);
+  SWARM_RTSTAMP(9);
 }
 
 // ---------------------------------------------------------------- slab reduction
@@ -450,8 +455,11 @@ struct ReduceArgs {
 // added in group order (fixed order -> bitwise reproducible run to run).
 constexpr int kRedCols = 16;
 constexpr int kRedGroups = 64;
-__global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(ReduceArgs A) {
+// slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start
+__global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(const float* slabs, swarm_ctrl* ctrl,
+                                                                            int n_slabs, int advance, ReduceArgs A) {
   __shared__ float part[kRedGroups][kRedCols];
+  SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
   const int c = threadIdx.x % kRedCols;
   const int col = blockIdx.x * kRedCols + c;
@@ -459,19 +467,19 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
   // advance mode: the thread owning column N_PARAMS is the control block's single writer.
   // It reads ctrl and prepares the whole update (incl. the double-precision Adam scalars
   // of the next step) before the slab loads return, and stores it at the end.
-  const bool writer = A.advance && col == N_PARAMS && q == 0;
-  const int per = (A.n_slabs + kRedGroups - 1) / kRedGroups;
-  const int b0 = q * per, b1 = min(A.n_slabs, b0 + per);
+  const bool writer = advance && col == N_PARAMS && q == 0;
+  const int per = (n_slabs + kRedGroups - 1) / kRedGroups;
+  const int b0 = q * per, b1 = min(n_slabs, b0 + per);
   // first chunk of this thread's slab column in flight before anything else
   constexpr int kChunk = 8;
   float v0[kChunk];
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
-    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? A.slabs[(size_t)(b0 + j) * (N_PARAMS + 1) + col] : 0.0f;
+    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[(size_t)(b0 + j) * (N_PARAMS + 1) + col] : 0.0f;
   // advance mode: the thread owning column N_PARAMS is the control block's single writer.
   // It prepares the whole update (incl. the double-precision Adam scalars of the next
   // step and the next tick's sampling key) while the slab loads fly, stores it at the end.
-  swarm_ctrl* C = A.ctrl;
+  swarm_ctrl* C = ctrl;
   uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
   double b1p = 1.0, b2p = 1.0;
   float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
@@ -488,7 +496,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
     }
   }
   // a second wave of the same block prepares the next tick's sampling key in parallel
-  const bool key_writer = A.advance && col == N_PARAMS && q == 4;
+  const bool key_writer = advance && col == N_PARAMS && q == 4;
   if (key_writer) {
     const uint32_t cap = (uint32_t)A.capacity;
     const uint32_t filled = C->filled_slots;
@@ -504,12 +512,12 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
     for (int b = b0 + kChunk; b < b1; b += kChunk) {
       float v[kChunk];
 #pragma unroll
-      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? A.slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
+      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
 #pragma unroll
       for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }
   }
-  if (A.advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
+  if (advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
     if (q == 0) A.lr.w_cur[col] = A.lr.w_nxt[col];
     else if (q == 1) A.lr.m_cur[col] = A.lr.m_nxt[col];
     else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
@@ -548,6 +556,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(Redu
     C->sample_tick = nk_tick;
   }
   SWARM_STAMP(31);
+  SWARM_RTSTAMP(23);
 }
 
 // ---------------------------------------------------------------- clip + Adam + target sync
@@ -673,9 +682,13 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.grad_scale = (float)(2.0 / ((double)hp->batch * (double)cfg->n_agents));
   const int nb = td_blocks(cfg, hp->batch);
   hipStream_t st = (hipStream_t)stream;
-  if (a.N <= 8) hipLaunchKernelGGL((td_kernel<16, 8>), dim3(nb), dim3(128 * 2), 0, st, a);
-  else if (a.N <= 16) hipLaunchKernelGGL((td_kernel<16, 16>), dim3(nb), dim3(128 * 2), 0, st, a);
-  else hipLaunchKernelGGL((td_kernel<32, 32>), dim3(nb), dim3(128), 0, st, a);
+#define SWARM_TD_LAUNCH(NS, GS, NT)                                                                       \
+  hipLaunchKernelGGL((td_kernel<NS, GS>), dim3(nb), dim3(NT), 0, st, a.sample_in, a.replay.s, a.replay.s_next, \
+                     a.replay.r, a.replay.a, a.S, a.B, a.N, a.replay.capacity, a)
+  if (a.N <= 8) SWARM_TD_LAUNCH(16, 8, 128 * 2);
+  else if (a.N <= 16) SWARM_TD_LAUNCH(16, 16, 128 * 2);
+  else SWARM_TD_LAUNCH(32, 32, 128);
+#undef SWARM_TD_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -689,7 +702,7 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
   ReduceArgs a = {};
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = grad;
   hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + kRedCols - 1) / kRedCols), dim3(kRedCols * kRedGroups), 0,
-                     (hipStream_t)stream, a);
+                     (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }
 
@@ -705,7 +718,7 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
   hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + kRedCols - 1) / kRedCols), dim3(kRedCols * kRedGroups), 0,
-                     (hipStream_t)stream, a);
+                     (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }
 
