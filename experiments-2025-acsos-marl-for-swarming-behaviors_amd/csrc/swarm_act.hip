@@ -45,7 +45,9 @@ constexpr int kActWPB = 4;   // waves (= environments) per act block; the block 
 // The first memory round trip's pointers and the geometry lead the parameter list so that
 // they arrive preloaded in SGPRs (kernarg preload, -amdgpu-kernarg-preload-count): the
 // prologue's loads issue at wave start instead of behind a kernarg-segment fetch.
-template <int NS, int MODE, int SCEN>   // SCEN: compile-time scenario (no speculated OA physics)
+// SCEN: compile-time scenario (no speculated OA physics).  FAST: complete graph + GAT fixed at
+// compile time — the headline configuration's kernel carries no kNN / dense / GCN code.
+template <int NS, int MODE, int SCEN, bool FAST>
 __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
                                                           const float* grad, const float* w_cur,
                                                           const float* m_cur, const float* v_cur, int B, int N,
@@ -58,6 +60,8 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __r
   SWARM_STAMP(0);
   const int w = threadIdx.x >> 6;
   const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * kActWPB + w, B);
+  const int graph = FAST ? (int)SWARM_GRAPH_COMPLETE : A.graph;
+  const int conv = FAST ? (int)SWARM_CONV_GAT : A.conv;
   const WView<NS> V = SW[w].view();
   WSmall<NS>& sm = SW[w].sm;
   const int c = d.c, p = d.p;
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __r
       }
     }
     if (MODE != MODE_STEP) {
-      dl_forward<NS, 8>(P, d, N, A.graph, A.k, A.conv, A.dense, V, false, F);
+      dl_forward<NS, 8>(P, d, N, graph, A.k, conv, A.dense, V, false, F);
     } else {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
@@ -259,9 +263,9 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __r
         if (MODE == MODE_TICK || MODE == MODE_STEP) {
           if (MODE == MODE_TICK && A.out.q)
             for (int a = p; a < kActions; a += 4) A.out.q[node[ct] * kActions + a] = sm.Q[n][a];
-          if (MODE == MODE_TICK && A.out.mult && A.graph != SWARM_GRAPH_DENSE)
+          if (MODE == MODE_TICK && A.out.mult && graph != SWARM_GRAPH_DENSE)
             for (int u = p; u < N; u += 4)
-              A.out.mult[((size_t)d.gid * N + u) * N + n] = (uint8_t)in_mult<NS>(u, n, N, A.graph, sm, nullptr, d.gid);
+              A.out.mult[((size_t)d.gid * N + u) * N + n] = (uint8_t)in_mult<NS>(u, n, N, graph, sm, nullptr, d.gid);
           if (p == 0) {
             if (A.out.actions) A.out.actions[node[ct]] = action[ct];
             if (o_rew) o_rew[node[ct]] = rew;
@@ -431,14 +435,19 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   if (tiles == 0) return 0;
   const dim3 grid((tiles + kActWPB - 1) / kActWPB), block(64 * kActWPB);
   const float *g = a.lr.grad, *w = a.lr.w_cur, *m = a.lr.m_cur, *v = a.lr.v_cur;
+#define SWARM_ACT_LAUNCH1(NS, SC, F) \
+  hipLaunchKernelGGL((act_kernel<NS, MODE, SC, F>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
 #define SWARM_ACT_LAUNCH(NS, SC) \
-  hipLaunchKernelGGL((act_kernel<NS, MODE, SC>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
+  do { if (fast) SWARM_ACT_LAUNCH1(NS, SC, kFastable); else SWARM_ACT_LAUNCH1(NS, SC, false); } while (0)
   constexpr int OA = (MODE == MODE_Q) ? SWARM_GOTO : SWARM_OBSTACLE_AVOIDANCE;   // MODE_Q has no physics
   const bool oa = MODE != MODE_Q && a.scenario == SWARM_OBSTACLE_AVOIDANCE;
+  constexpr bool kFastable = MODE == MODE_TICK || MODE == MODE_ROLLOUT;
+  const bool fast = kFastable && a.graph == SWARM_GRAPH_COMPLETE && a.conv == SWARM_CONV_GAT;
   if (a.N <= 8) { if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO); }
   else if (a.N <= 16) { if (oa) SWARM_ACT_LAUNCH(16, OA); else SWARM_ACT_LAUNCH(16, SWARM_GOTO); }
   else { if (oa) SWARM_ACT_LAUNCH(32, OA); else SWARM_ACT_LAUNCH(32, SWARM_GOTO); }
 #undef SWARM_ACT_LAUNCH
+#undef SWARM_ACT_LAUNCH1
   return (int)hipGetLastError();
 }
 
