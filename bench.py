@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
+                    "gloo only to rehearse several ranks on one GPU)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="rehearsal: create the process group and run the gradient all-reduce even at 1 rank")
     return ap.parse_args()
 
 
@@ -77,14 +81,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))   # several gloo ranks may share a GPU
+    distributed = world > 1 or args.force_dist
     import swarm_amd
     from swarm_amd import dist as swdist
-    pg = swdist.init_process_group("nccl", local_rank) if world > 1 else None
+    pg = swdist.init_process_group(args.backend, local_rank) if distributed else None
     from swarm_amd import build as swbuild
     if rank == 0 and not swbuild.up_to_date():
         swbuild.build()
-    if world > 1:
+    if distributed:
         torch.distributed.barrier()
 
     B, N = args.envs, args.agents
@@ -110,9 +115,18 @@ def main():
 
     chunk = max(1, math.gcd(args.steps, args.chunk)) if args.steps else 1
     graph = None
-    if not args.no_graph and world == 1:
-        tick()                              # eager warm tick before capture
-        graph = eng.capture(chunk, tick)
+    if not args.no_graph and (not distributed or args.backend == "nccl"):
+        tick()                              # eager warm tick (and first RCCL all-reduce) before capture
+        try:
+            graph = eng.capture(chunk, tick)
+        except RuntimeError as e:           # e.g. a collective that refuses stream capture
+            print(f"[bench] rank {rank}: hipGraph capture failed ({e}); eager ticks", file=sys.stderr)
+            graph = None
+        if distributed:                     # every rank runs the same launch mode
+            ok = torch.tensor([1 if graph is not None else 0], device="cuda", dtype=torch.int32)
+            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                graph = None
 
     def run(n):
         done = 0
@@ -131,22 +145,34 @@ def main():
 
     run(args.warmup)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     ctrl = eng.read_ctrl()
     assert ctrl["trained"] == 1 and math.isfinite(ctrl["loss"]), ctrl
+    replicas = None
+    if distributed:
+        # data-parallel invariant: after the same all-reduced updates every replica's weights,
+        # moments and target are bitwise identical (min == max over ranks, element by element)
+        eng.flush()
+        st = torch.cat([eng.params, eng.adam_m, eng.adam_v, eng.target])
+        lo, hi = st.clone(), st.clone()
+        torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
+        torch.distributed.all_reduce(hi, op=torch.distributed.ReduceOp.MAX)
+        replicas = bool(torch.equal(lo, hi))
+        if not replicas:
+            raise SystemExit(f"rank {rank}: replicas diverged after {args.steps} ticks")
 
     # ---- per-kernel durations: each kernel of the fused tick as a captured chain of KCHAIN
     #      back-to-back launches (the same inputs every launch: TD and the slab reduce are pure
@@ -215,12 +241,12 @@ def main():
                 "config": {"workload": f"{scen} train tick: {N} agents x {B} envs/GPU, GAT, complete graph, "
                                        f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
                            "global_envs": B * world, "td_batch_per_gpu": S, "graph": "complete",
-                           "parallelism": f"env-sharded dp{world}" + (" + RCCL grad all-reduce" if world > 1 else ""),
-                           "hipgraph": graph is not None},
+                           "parallelism": f"env-sharded dp{world}" + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce" if distributed else ""),
+                           "hipgraph": graph is not None, "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu,
                 "loss": ctrl["loss"]}
         print(json.dumps(line))
-    if world > 1:
+    if distributed:
         torch.distributed.destroy_process_group()
 
 

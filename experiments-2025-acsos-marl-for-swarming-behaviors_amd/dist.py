@@ -60,9 +60,9 @@ def init_process_group(backend: str, local_rank: Optional[int] = None):
 
 
 def allreduce_grad_(grad: torch.Tensor, world_size: int, group=None) -> torch.Tensor:
-    """In-place SUM of the flat gradient over ranks (no-op for one rank).  The
-    division by W happens inside the optimizer step (swarm_adam_cfg.world_size)."""
-    if world_size > 1:
+    """In-place SUM of the flat gradient over ranks (no-op for one rank without a group).
+    The division by W happens inside the optimizer step (swarm_adam_cfg.world_size)."""
+    if world_size > 1 or group is not None:
         import torch.distributed as dist
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
     return grad

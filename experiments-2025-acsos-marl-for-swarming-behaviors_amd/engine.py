@@ -270,13 +270,16 @@ class SwarmEngine:
 
     # ------------------------------------------------------------------ hipGraph
     def capture(self, n_ticks: int, fn=None):
-        """Capture n_ticks calls of ``fn`` (default train_tick) into one hipGraph."""
+        """Capture n_ticks calls of ``fn`` (default train_tick) into one hipGraph.  With
+        world_size > 1 the tick's RCCL all-reduce is captured too; the capture is then
+        thread-local so the process group's watchdog thread may keep querying its events."""
         fn = fn or self.train_tick
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
         graph = torch.cuda.CUDAGraph()
+        mode = "thread_local" if self.world_size > 1 else "global"
         with torch.cuda.stream(s):
-            with torch.cuda.graph(graph, stream=s):
+            with torch.cuda.graph(graph, stream=s, capture_error_mode=mode):
                 for _ in range(n_ticks):
                     fn()
         torch.cuda.current_stream().wait_stream(s)
