@@ -49,6 +49,16 @@ def td_bwd_flops(N: int, d: float) -> float:
             + 32 * 3 + 9)              # dbias, db1, db2
 
 
+def gcn_fwd_flops(N: int, d: float) -> float:
+    """GCNConv variant (a13) per node: lin 7->32 (448), normalised aggregate (64/edge + 3/edge
+    coefficients), bias+tanh (64), lin1, relu, lin2 as for the GAT."""
+    return 448 + 67 * d + 64 + 2080 + 32 + 585
+
+
+def gcn_bwd_flops(N: int, d: float) -> float:
+    return 32 + 32 + 2048 + 96 + 64 * d + 2048 + 64 + 448 + 32 * 2 + 9
+
+
 def complete_in_degree(N: int) -> float:
     return ((N - 1) * N + 1) / N
 
@@ -61,6 +71,12 @@ def parse():
     ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--scenario", default="GoTo")
+    ap.add_argument("--conv", default="gat", choices=("gat", "gcn"))
+    ap.add_argument("--graph", default="complete", choices=("complete", "knn"))
+    ap.add_argument("--knn-k", type=int, default=10)
+    ap.add_argument("--mode", default="train", choices=("train", "act"),
+                    help="train: fused training tick (headline); act: acting-only rollout with frozen "
+                         "weights, eps 0 (Simulator-shaped, replicas only)")
     ap.add_argument("--batch", type=int, default=None, help="sampled graphs per update per GPU (default = envs)")
     ap.add_argument("--chunk", type=int, default=20, help="ticks per captured hipGraph")
     ap.add_argument("--no-graph", action="store_true")
@@ -100,8 +116,10 @@ def main():
     w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
     eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=shard.env_offset,
                                 world_size=world, process_group=pg, update_target_every=200,
-                                replay_capacity=1_000_000)
+                                replay_capacity=1_000_000, conv=args.conv, graph=args.graph, knn_k=args.knn_k)
     max_steps = 100
+    if args.mode == "act":
+        return bench_act(args, eng, world, rank, distributed, max_steps)
     # ---- prefill: 100 acting ticks (no learning)
     eng.reset()
     for _ in range(100):
@@ -199,16 +217,18 @@ def main():
 
     value = B * N * world * args.steps / elapsed
     ms = elapsed / args.steps * 1e3
-    d = complete_in_degree(N)
-    f_fwd = gat_fwd_flops(N, d)
-    td_flops_launch = S * N * (2 * f_fwd + td_bwd_flops(N, d))
+    d = complete_in_degree(N) if args.graph == "complete" else (2 * N * args.knn_k + 1) / N
+    if args.conv == "gat":
+        td_flops_launch = S * N * (2 * gat_fwd_flops(N, d) + td_bwd_flops(N, d))
+    else:
+        td_flops_launch = S * N * (2 * gcn_fwd_flops(N, d) + gcn_bwd_flops(N, d))
     roof = None
     if kt:
         t_td = kt["td_kernel"] * 1e-6
         ach = td_flops_launch / t_td / 1e12
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "r01_pmc_td.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and (scen, N, B, S, args.conv, args.graph) == ("GoTo", 8, 1024, 1024, "gat", "complete"):
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": "td_kernel (swarm_td_grad)",
@@ -238,13 +258,83 @@ def main():
                 "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference GoTo seed_0 weights)",
-                "config": {"workload": f"{scen} train tick: {N} agents x {B} envs/GPU, GAT, complete graph, "
+                "config": {"workload": f"{scen} train tick: {N} agents x {B} envs/GPU, {args.conv.upper()}, "
+                                       f"{args.graph if args.graph == 'complete' else f'kNN-{args.knn_k}'} graph, "
                                        f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
-                           "global_envs": B * world, "td_batch_per_gpu": S, "graph": "complete",
+                           "global_envs": B * world, "td_batch_per_gpu": S, "graph": args.graph, "conv": args.conv,
                            "parallelism": f"env-sharded dp{world}" + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce" if distributed else ""),
                            "hipgraph": graph is not None, "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu,
                 "loss": ctrl["loss"]}
+        print(json.dumps(line))
+    if distributed:
+        torch.distributed.destroy_process_group()
+
+
+def bench_act(args, eng, world, rank, distributed, max_steps):
+    """Acting-only throughput (SURVEY §8(d) "acting-only": S = 0, frozen weights, like
+    Simulator.run_simulation): graph -> GAT/GCN Q -> argmax -> env.step for every env, episodes of
+    max_steps ticks, each episode ONE swarm_rollout launch (weights staged once, state kept in
+    registers across ticks).  No collective: N > 1 runs independent replicas."""
+    B, N = args.envs, args.agents
+
+    def run(n):
+        done, t_ep = 0, 0
+        eng.reset()
+        while done < n:
+            if t_ep >= max_steps:
+                eng.reset()
+                t_ep = 0
+            m = min(max_steps - t_ep, n - done)
+            eng.rollout(m, tick0=done, eps=0.0)
+            done += m
+            t_ep += m
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    if distributed:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if distributed:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    d = complete_in_degree(N) if args.graph == "complete" else (2 * N * args.knn_k + 1) / N
+    f_node = (gat_fwd_flops(N, d) if args.conv == "gat" else gcn_fwd_flops(N, d)) + 300   # + physics
+    roof = None
+    if not args.no_kernel_timing:   # one 100-tick rollout launch, HIP events on its stream
+        stream = torch.cuda.current_stream()
+        per = []
+        for _ in range(5):
+            eng.reset()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            eng.rollout(max_steps, eps=0.0)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            per.append(e0.elapsed_time(e1) * 1e-3)
+        t_l = float(np.median(per))
+        flops = B * N * max_steps * f_node
+        ach = flops / t_l / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP32_TFLOPS, "traffic": None, "kernel": "act_kernel rollout (swarm_rollout)",
+                "algorithmic_flops_per_launch": flops, "launch_us": round(t_l * 1e6, 2)}
+    if rank == 0:
+        g = args.graph if args.graph == "complete" else f"kNN-{args.knn_k}"
+        line = {"metric": "env-steps/sec (agents×envs), acting-only rollout", "value": round(B * N * world * args.steps / elapsed, 1),
+                "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference seed_0 weights)",
+                "config": {"workload": f"{args.scenario} acting-only: {N} agents x {B} envs/GPU, {args.conv.upper()}, "
+                                       f"{g} graph, eps 0, frozen weights", "envs_per_gpu": B, "agents": N,
+                           "global_envs": B * world, "graph": args.graph, "conv": args.conv,
+                           "parallelism": f"replicas x{world}"},
+                "roofline": roof, "cpu_baseline": None}
         print(json.dumps(line))
     if distributed:
         torch.distributed.destroy_process_group()

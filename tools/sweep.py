@@ -1,0 +1,43 @@
+"""Bench lines for the BASELINE.json configs beside the headline (C3, the per-GPU share of C5, and
+acting-only rollouts), one bench.py subprocess each, appended to a JSON-lines file.
+
+    python tools/sweep.py [out.jsonl]
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "sweep.jsonl")
+COMMON = ["--no-cpu-baseline", "--steps", "200", "--warmup", "10"]
+
+RUNS = [("C3 OA 12x1024 GAT train", ["--scenario", "ObstacleAvoidance", "--agents", "12"])]
+# C5 per GPU: 4096 envs over 8 GPUs = 512 envs/GPU, N = 5..12, GCN vs GAT
+for conv in ("gat", "gcn"):
+    for n in range(5, 13):
+        RUNS.append((f"C5 OA {n}x512 {conv.upper()} train",
+                     ["--scenario", "ObstacleAvoidance", "--agents", str(n), "--envs", "512", "--conv", conv]))
+RUNS += [
+    ("C2 GoTo 8x1024 GCN train", ["--conv", "gcn"]),
+    ("C2 GoTo 8x1024 GAT act kNN-5", ["--mode", "act", "--graph", "knn", "--knn-k", "5"]),
+    ("C2 GoTo 8x1024 GAT act complete", ["--mode", "act"]),
+    ("C3 OA 12x1024 GAT act kNN-10", ["--mode", "act", "--scenario", "ObstacleAvoidance", "--agents", "12",
+                                      "--graph", "knn", "--knn-k", "10"]),
+]
+
+os.makedirs(os.path.dirname(OUT), exist_ok=True)
+with open(OUT, "w") as f:
+    for name, extra in RUNS:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + COMMON + extra
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+        if p.returncode != 0:
+            print(f"{name}: rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
+            sys.exit(p.returncode)
+        line = json.loads(p.stdout.strip().splitlines()[-1])
+        line["sweep"] = name
+        f.write(json.dumps(line) + "\n")
+        f.flush()
+        r = line.get("roofline") or {}
+        print(f"{name:40s} {line['value'] / 1e6:9.1f} M agent-steps/s  {line['ms_per_step'] * 1e3:7.2f} us/step  "
+              f"frac={r.get('frac', float('nan')):.4f}", flush=True)
