@@ -371,6 +371,7 @@ __global__ void reset_kernel(int B, int N, int scenario, int flags, uint32_t k0,
 template <int NS>
 __global__ __launch_bounds__(64) void graph_kernel(ActArgs A, uint8_t* __restrict__ mult_out) {
   __shared__ WSmall<NS> sm;
+  __shared__ KV kq[NS][NS];   // per-slot work space of the kNN tie path
   const int N = A.N;
   const WGeom<NS> g = make_wgeom<NS>(blockIdx.x, A.B, N);
   const size_t node = (size_t)g.gid * N + (g.valid ? g.s : 0);
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(64) void graph_kernel(ActArgs A, uint8_t* __restric
   }
   wave_lds_sync();
   if (A.graph == SWARM_GRAPH_KNN) {
-    const uint32_t m = g.valid ? knn_mask<NS>(g, N, A.k, sm) : 0u;
+    const uint32_t m = g.valid ? knn_mask<NS>(g, N, A.k, sm, kq[g.s]) : 0u;
     if (g.q == 0) sm.knn[g.s] = m;
     wave_lds_sync();
   }

@@ -112,15 +112,16 @@ __device__ inline void in_mults(int n, int N, int graph, const WSmall<NS>& sm, c
   }
 }
 
-// kNN row of slot n over its graph (positions in sm; bit j = local node j)
+// kNN row of slot n over its graph (positions in sm; bit j = local node j).  q: GS
+// entries of lane-private LDS for the boundary-tie path.
 template <int NS, int GS = NS>
-__device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& sm) {
+__device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& sm, KV* q) {
   float d[GS];
   const int base = (GS < NS) ? (n / GS) * GS : 0;
   const float xi = sm.px[n], yi = sm.py[n];
 #pragma unroll
   for (int j = 0; j < GS; ++j) d[j] = (j < N) ? norm2(sm.px[base + j] - xi, sm.py[base + j] - yi) : 0.0f;
-  return topk_smallest_mask<GS>(d, N, k);
+  return topk_smallest_mask<GS>(d, N, k, q);
 }
 
 // Full GCN.forward.  F.x must hold the lane's features (zero for nodes >= N).  P is the
@@ -189,7 +190,10 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c;
-      if (n < NS && p == 0) sm.knn[n] = (((GS < NS) ? n % GS : n) < N) ? knn_mask_node<NS, GS>(n, N, k, sm) : 0u;
+      // tie-path work space: node n's GS entries in the wave's T / R rows (contiguous,
+      // free until the aggregation writes T; 2 NS kRow floats >= 2 NS GS)
+      KV* q = reinterpret_cast<KV*>(&V.T[0][0]) + (n < NS ? n : 0) * GS;
+      if (n < NS && p == 0) sm.knn[n] = (((GS < NS) ? n % GS : n) < N) ? knn_mask_node<NS, GS>(n, N, k, sm, q) : 0u;
     }
     wave_lds_sync();
   }

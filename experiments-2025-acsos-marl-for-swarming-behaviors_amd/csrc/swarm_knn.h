@@ -121,27 +121,37 @@ __host__ __device__ inline void kv_nth_element(KV* a, int n, int nth) {
   kv_insertion_sort(a, first, last);
 }
 
-// selection bitmask over j < n (n <= 32) of torch.topk(d, k, largest=False) on CPU
+// selection bitmask over j < n (n <= 32) of torch.topk(d, k, largest=False) on CPU.
+// q: NMAX entries of work space for the tie path; on the device the callers pass a
+// lane-private slice of LDS (a private array with data-dependent indices lives in
+// scratch memory, one HBM round trip per introselect step).
 template <int NMAX>
-__host__ __device__ inline uint32_t topk_smallest_mask(const float* d, int n, int k) {
+__host__ __device__ inline uint32_t topk_smallest_mask(const float* d, int n, int k, KV* q) {
   uint32_t mask = 0;
   int count = 0;
+#pragma unroll
   for (int j = 0; j < NMAX; ++j) {
-    if (j >= n) break;
-    int lt = 0;
-    for (int l = 0; l < NMAX; ++l) {
-      if (l >= n) break;
-      lt += d[l] < d[j] ? 1 : 0;
+    if (j < n) {
+      int lt = 0;
+#pragma unroll
+      for (int l = 0; l < NMAX; ++l) lt += (l < n && d[l] < d[j]) ? 1 : 0;
+      if (lt < k) { mask |= 1u << j; ++count; }
     }
-    if (lt < k) { mask |= 1u << j; ++count; }
   }
   if (count == k) return mask;
-  KV q[NMAX];
-  for (int j = 0; j < n; ++j) { q[j].v = d[j]; q[j].i = j; }
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j)
+    if (j < n) { q[j].v = d[j]; q[j].i = j; }
   kv_nth_element(q, n, k - 1);
   mask = 0;
   for (int j = 0; j < k; ++j) mask |= 1u << q[j].i;
   return mask;
+}
+
+template <int NMAX>
+__host__ __device__ inline uint32_t topk_smallest_mask(const float* d, int n, int k) {
+  KV q[NMAX];
+  return topk_smallest_mask<NMAX>(d, n, k, q);
 }
 
 }  // namespace swarm

@@ -162,12 +162,12 @@ template <int NS> struct Dl { static constexpr int CT = (NS + 15) / 16; };
 
 // kNN row of slot s over the graph (simulator.py:17-19 -> CPU torch.topk set semantics)
 template <int NS>
-__device__ inline uint32_t knn_mask(const WGeom<NS>& g, int N, int k, const WSmall<NS>& sm) {
+__device__ inline uint32_t knn_mask(const WGeom<NS>& g, int N, int k, const WSmall<NS>& sm, KV* q) {
   float d[NS];
   const float xi = sm.px[g.s], yi = sm.py[g.s];
 #pragma unroll
   for (int j = 0; j < NS; ++j) d[j] = (j < N) ? norm2(sm.px[j] - xi, sm.py[j] - yi) : 0.0f;
-  return topk_smallest_mask<NS>(d, N, k);
+  return topk_smallest_mask<NS>(d, N, k, q);
 }
 
 // multiplicity m(u -> s) of every source slot u (target = this lane's slot)

@@ -1,7 +1,7 @@
 """Bench lines for the BASELINE.json configs beside the headline (C3, the per-GPU share of C5, and
 acting-only rollouts), one bench.py subprocess each, appended to a JSON-lines file.
 
-    python tools/sweep.py [out.jsonl]
+    python tools/sweep.py [out.jsonl] [substring filter on the run names]
 """
 import json
 import os
@@ -26,6 +26,8 @@ RUNS += [
                                       "--graph", "knn", "--knn-k", "10"]),
 ]
 
+if len(sys.argv) > 2:
+    RUNS = [r for r in RUNS if sys.argv[2] in r[0]]
 os.makedirs(os.path.dirname(OUT), exist_ok=True)
 with open(OUT, "w") as f:
     for name, extra in RUNS:
