@@ -41,10 +41,21 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> st
     if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _deps()):
         return out
     extra = ["-DSWARM_STAMPS=1"] if stamps else []
-    cmd = [HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
-    if verbose:
-        print("[build]", " ".join(cmd), file=sys.stderr)
+    # one hipcc process per translation unit (in parallel), then one link
+    objs = [f"{out}.{os.path.splitext(src)[0]}.o" for src in SOURCES]
+    cflags = [f for f in FLAGS if f != "-shared"]
+    procs = []
+    for src, obj in zip(SOURCES, objs):
+        cmd = [HIPCC, *cflags, *extra, "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print("[build]", " ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out + ".tmp", *objs]
     subprocess.run(cmd, check=True)
+    for obj in objs:
+        os.remove(obj)
     os.replace(out + ".tmp", out)
     return out
 

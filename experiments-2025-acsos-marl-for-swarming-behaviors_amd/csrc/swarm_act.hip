@@ -45,9 +45,10 @@ constexpr int kActWPB = 4;   // waves (= environments) per act block; the block 
 // The first memory round trip's pointers and the geometry lead the parameter list so that
 // they arrive preloaded in SGPRs (kernarg preload, -amdgpu-kernarg-preload-count): the
 // prologue's loads issue at wave start instead of behind a kernarg-segment fetch.
-// SCEN: compile-time scenario (no speculated OA physics).  FAST: complete graph + GAT fixed at
-// compile time — the headline configuration's kernel carries no kNN / dense / GCN code.
-template <int NS, int MODE, int SCEN, bool FAST>
+// SCEN: compile-time scenario (no speculated OA physics).  SPEC fixes graph and conv at
+// compile time (SPEC_* in swarm_common.h) — e.g. the headline configuration's kernel
+// (complete + GAT) carries no kNN / dense / GCN code; SPEC_RUNTIME reads them from A.
+template <int NS, int MODE, int SCEN, int SPEC>
 __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
                                                           const float* grad, const float* w_cur,
                                                           const float* m_cur, const float* v_cur, int B, int N,
@@ -60,8 +61,8 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __r
   SWARM_STAMP(0);
   const int w = threadIdx.x >> 6;
   const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * kActWPB + w, B);
-  const int graph = FAST ? (int)SWARM_GRAPH_COMPLETE : A.graph;
-  const int conv = FAST ? (int)SWARM_CONV_GAT : A.conv;
+  const int graph = spec_graph<SPEC>(A.graph);
+  const int conv = spec_conv<SPEC>(A.conv);
   const WView<NS> V = SW[w].view();
   WSmall<NS>& sm = SW[w].sm;
   const int c = d.c, p = d.p;
@@ -436,14 +437,24 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   if (tiles == 0) return 0;
   const dim3 grid((tiles + kActWPB - 1) / kActWPB), block(64 * kActWPB);
   const float *g = a.lr.grad, *w = a.lr.w_cur, *m = a.lr.m_cur, *v = a.lr.v_cur;
-#define SWARM_ACT_LAUNCH1(NS, SC, F) \
-  hipLaunchKernelGGL((act_kernel<NS, MODE, SC, F>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
-#define SWARM_ACT_LAUNCH(NS, SC) \
-  do { if (fast) SWARM_ACT_LAUNCH1(NS, SC, kFastable); else SWARM_ACT_LAUNCH1(NS, SC, false); } while (0)
+  // specialised kernels for the training tick (complete graph, GAT or GCN) and the rollout
+  // (those two plus kNN + GAT, the Simulator's graph); everything else runs SPEC_RUNTIME
+  constexpr bool kTick = MODE == MODE_TICK || MODE == MODE_ROLLOUT;
+  constexpr int S1 = kTick ? SPEC_COMPLETE_GAT : SPEC_RUNTIME;
+  constexpr int S2 = kTick ? SPEC_COMPLETE_GCN : SPEC_RUNTIME;
+  constexpr int S3 = MODE == MODE_ROLLOUT ? SPEC_KNN_GAT : SPEC_RUNTIME;
+  const int spec = kTick ? spec_of(a.graph, a.conv) : SPEC_RUNTIME;
+#define SWARM_ACT_LAUNCH1(NS, SC, SP) \
+  hipLaunchKernelGGL((act_kernel<NS, MODE, SC, SP>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
+#define SWARM_ACT_LAUNCH(NS, SC)                                  \
+  do {                                                            \
+    if (spec == SPEC_COMPLETE_GAT) SWARM_ACT_LAUNCH1(NS, SC, S1);  \
+    else if (spec == SPEC_COMPLETE_GCN) SWARM_ACT_LAUNCH1(NS, SC, S2); \
+    else if (spec == SPEC_KNN_GAT) SWARM_ACT_LAUNCH1(NS, SC, S3);  \
+    else SWARM_ACT_LAUNCH1(NS, SC, SPEC_RUNTIME);                  \
+  } while (0)
   constexpr int OA = (MODE == MODE_Q) ? SWARM_GOTO : SWARM_OBSTACLE_AVOIDANCE;   // MODE_Q has no physics
   const bool oa = MODE != MODE_Q && a.scenario == SWARM_OBSTACLE_AVOIDANCE;
-  constexpr bool kFastable = MODE == MODE_TICK || MODE == MODE_ROLLOUT;
-  const bool fast = kFastable && a.graph == SWARM_GRAPH_COMPLETE && a.conv == SWARM_CONV_GAT;
   if (a.N <= 8) { if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO); }
   else if (a.N <= 16) { if (oa) SWARM_ACT_LAUNCH(16, OA); else SWARM_ACT_LAUNCH(16, SWARM_GOTO); }
   else { if (oa) SWARM_ACT_LAUNCH(32, OA); else SWARM_ACT_LAUNCH(32, SWARM_GOTO); }

@@ -231,4 +231,20 @@ static __constant__ unsigned long long* g_swarm_stamps;
   } while (0)
 #endif
 
+// compile-time graph / conv specialisations of the act and TD kernels
+enum { SPEC_RUNTIME = 0, SPEC_COMPLETE_GAT = 1, SPEC_COMPLETE_GCN = 2, SPEC_KNN_GAT = 3 };
+__host__ __device__ inline int spec_of(int graph, int conv) {
+  if (graph == SWARM_GRAPH_COMPLETE) return conv == SWARM_CONV_GAT ? SPEC_COMPLETE_GAT : SPEC_COMPLETE_GCN;
+  if (graph == SWARM_GRAPH_KNN && conv == SWARM_CONV_GAT) return SPEC_KNN_GAT;
+  return SPEC_RUNTIME;
+}
+template <int SPEC>
+__device__ inline int spec_graph(int runtime) {
+  return SPEC == SPEC_RUNTIME ? runtime : (SPEC == SPEC_KNN_GAT ? (int)SWARM_GRAPH_KNN : (int)SWARM_GRAPH_COMPLETE);
+}
+template <int SPEC>
+__device__ inline int spec_conv(int runtime) {
+  return SPEC == SPEC_RUNTIME ? runtime : (SPEC == SPEC_COMPLETE_GCN ? (int)SWARM_CONV_GCN : (int)SWARM_CONV_GAT);
+}
+
 }  // namespace swarm

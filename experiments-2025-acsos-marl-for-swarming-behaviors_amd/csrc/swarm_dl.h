@@ -124,6 +124,48 @@ __device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& 
   return topk_smallest_mask<GS>(d, N, k, q);
 }
 
+// kNN rows of every slot of the wave at once (NS <= 16): lane l serves slot n = l / LPN and
+// the candidates j = l % LPN + LPN i of n's graph.  Each pair distance is computed once
+// (the same fp32 expression as knn_mask_node), the graph's distance rows meet in LDS
+// (dn), and the set {j : #{l : d_l < d_j} < k} is assembled from wave ballots.  A slot
+// whose count test fails (a boundary tie) runs the introselect emulation in lane r = 0
+// with its work space in LDS (q).  Writes sm.knn[n].
+template <int NS, int GS>
+__device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, float* __restrict__ dn, KV* q) {
+  constexpr int LPN = 64 / NS;          // lanes per slot
+  constexpr int CPL = GS / LPN;         // candidates per lane
+  static_assert(CPL >= 1 && GS % LPN == 0, "knn_masks_wave geometry");
+  const int n = lane / LPN, r = lane % LPN;
+  const int base = (GS < NS) ? (n / GS) * GS : 0;
+  const int jn = (GS < NS) ? n % GS : n;
+  const bool nvalid = jn < N;
+  const float xi = sm.px[n], yi = sm.py[n];
+  float dv[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int j = r + LPN * i;
+    dv[i] = (j < N) ? norm2(sm.px[base + j] - xi, sm.py[base + j] - yi) : 0.0f;
+    dn[n * GS + j] = dv[i];
+  }
+  wave_lds_sync();
+  float row[GS];
+  lds_load<GS>(dn + n * GS, row);
+  uint32_t mask = 0;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int j = r + LPN * i;
+    int lt = 0;
+#pragma unroll
+    for (int l = 0; l < GS; ++l) lt += (l < N && row[l] < dv[i]) ? 1 : 0;
+    const uint64_t b = __ballot(nvalid && j < N && lt < k);
+    mask |= (uint32_t)((b >> (n * LPN)) & ((1ull << LPN) - 1ull)) << (LPN * i);
+  }
+  if (r == 0) {
+    if (nvalid && __popc(mask) != k) mask = topk_tie_mask<GS>(row, N, k, q + n * GS);
+    sm.knn[n] = nvalid ? mask : 0u;
+  }
+}
+
 // Full GCN.forward.  F.x must hold the lane's features (zero for nodes >= N).  P is the
 // padded LDS weight image.  Writes the H rows (and T / R rows if keep_tr) of V, the
 // per-node scalars of V.sm, and leaves F.t / F.zr / F.cf / F.q for the backward.
@@ -187,13 +229,17 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
   wave_lds_sync();
   DF_STAMP(0);
   if (graph == SWARM_GRAPH_KNN) {
+    // work space in the wave's T / R rows (free until the aggregation writes T)
+    if constexpr (NS <= 16) {
+      knn_masks_wave<NS, GS>(d.lane, N, k, sm, &V.T[0][0], reinterpret_cast<KV*>(&V.R[0][0]));
+    } else {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int n = 16 * ct + c;
-      // tie-path work space: node n's GS entries in the wave's T / R rows (contiguous,
-      // free until the aggregation writes T; 2 NS kRow floats >= 2 NS GS)
-      KV* q = reinterpret_cast<KV*>(&V.T[0][0]) + (n < NS ? n : 0) * GS;
-      if (n < NS && p == 0) sm.knn[n] = (((GS < NS) ? n % GS : n) < N) ? knn_mask_node<NS, GS>(n, N, k, sm, q) : 0u;
+      for (int ct = 0; ct < CT; ++ct) {
+        const int n = 16 * ct + c;
+        // node n's GS entries of T / R (contiguous: 2 NS kRow floats >= 2 NS GS)
+        KV* q = reinterpret_cast<KV*>(&V.T[0][0]) + (n < NS ? n : 0) * GS;
+        if (n < NS && p == 0) sm.knn[n] = (((GS < NS) ? n % GS : n) < N) ? knn_mask_node<NS, GS>(n, N, k, sm, q) : 0u;
+      }
     }
     wave_lds_sync();
   }

@@ -148,6 +148,18 @@ __host__ __device__ inline uint32_t topk_smallest_mask(const float* d, int n, in
   return mask;
 }
 
+// the boundary-tie path alone (callers that already know the count test failed)
+template <int NMAX>
+__host__ __device__ inline uint32_t topk_tie_mask(const float* d, int n, int k, KV* q) {
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j)
+    if (j < n) { q[j].v = d[j]; q[j].i = j; }
+  kv_nth_element(q, n, k - 1);
+  uint32_t mask = 0;
+  for (int j = 0; j < k; ++j) mask |= 1u << q[j].i;
+  return mask;
+}
+
 template <int NMAX>
 __host__ __device__ inline uint32_t topk_smallest_mask(const float* d, int n, int k) {
   KV q[NMAX];

@@ -87,7 +87,7 @@ __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*B
 // N <= 8 graphs into one wave: every MFMA column is a real node, one wave per SIMD).
 // The dependent chain's pointers (batch indices -> replay rows) and the geometry lead the
 // parameter list: preloaded into SGPRs (kernarg preload), the index loads issue at wave start.
-template <int NS, int GS, bool FAST>   // FAST: complete graph + GAT fixed at compile time
+template <int NS, int GS, int SPEC>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(const int32_t* sample_in, const float* rs, const float* rs_next,
                                                                        const float* rr, const uint8_t* ra, int S, int B, int N,
                                                                        int capacity, TdArgs A) {
@@ -101,8 +101,8 @@ __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(const int32_t*
   const bool online = wave < GPB;
   const int wi = online ? wave : wave - GPB;
   const DGeom<NS> d = make_dgeom<NS>(blockIdx.x * GPB + wi, 1 << 30);   // lane geometry; liveness is per graph
-  const int graph = FAST ? (int)SWARM_GRAPH_COMPLETE : A.graph;
-  const int conv = FAST ? (int)SWARM_CONV_GAT : A.conv;
+  const int graph = spec_graph<SPEC>(A.graph);
+  const int conv = spec_conv<SPEC>(A.conv);
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
   const int lane = d.lane, c = d.c, p = d.p;
@@ -696,12 +696,16 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.grad_scale = (float)(2.0 / ((double)hp->batch * (double)cfg->n_agents));
   const int nb = td_blocks(cfg, hp->batch);
   hipStream_t st = (hipStream_t)stream;
-  const bool fast = a.graph == SWARM_GRAPH_COMPLETE && a.conv == SWARM_CONV_GAT;
-#define SWARM_TD_LAUNCH1(NS, GS, NT, F)                                                                       \
-  hipLaunchKernelGGL((td_kernel<NS, GS, F>), dim3(nb), dim3(NT), 0, st, a.sample_in, a.replay.s, a.replay.s_next, \
+  const int spec = spec_of(a.graph, a.conv);   // training graphs are complete: GAT and GCN specialised
+#define SWARM_TD_LAUNCH1(NS, GS, NT, SP)                                                                       \
+  hipLaunchKernelGGL((td_kernel<NS, GS, SP>), dim3(nb), dim3(NT), 0, st, a.sample_in, a.replay.s, a.replay.s_next, \
                      a.replay.r, a.replay.a, a.S, a.B, a.N, a.replay.capacity, a)
-#define SWARM_TD_LAUNCH(NS, GS, NT) \
-  do { if (fast) SWARM_TD_LAUNCH1(NS, GS, NT, true); else SWARM_TD_LAUNCH1(NS, GS, NT, false); } while (0)
+#define SWARM_TD_LAUNCH(NS, GS, NT)                                                       \
+  do {                                                                                    \
+    if (spec == SPEC_COMPLETE_GAT) SWARM_TD_LAUNCH1(NS, GS, NT, SPEC_COMPLETE_GAT);      \
+    else if (spec == SPEC_COMPLETE_GCN) SWARM_TD_LAUNCH1(NS, GS, NT, SPEC_COMPLETE_GCN); \
+    else SWARM_TD_LAUNCH1(NS, GS, NT, SPEC_RUNTIME);                                      \
+  } while (0)
   if (a.N <= 8) SWARM_TD_LAUNCH(16, 8, 128 * 2);
   else if (a.N <= 16) SWARM_TD_LAUNCH(16, 16, 128 * 2);
   else SWARM_TD_LAUNCH(32, 32, 128);

@@ -495,12 +495,15 @@ def complete_batch_edge_index(S: int, N: int) -> torch.Tensor:
 
 
 def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma=0.99,
-                 edge_index=None, edge_index_next=None):
+                 edge_index=None, edge_index_next=None, conv: str = "gat"):
     """TD loss and its gradient (train_gcn_dqn.py:113-124) on S sampled graphs of N nodes.
 
     s_state / s_next_state: [S,N,4] (pos, vel); actions [S,N] int; rewards [S,N].
+    conv="gcn": the a13 GCNConv variant (parity unpinned) on complete graphs.
     Returns (loss, flat grad [N_PARAMS], online Q at the taken actions, TD targets).
     """
+    if conv == "gcn":
+        return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma)
     S, N, _ = s_state.shape
     params = {k: v.clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
     tparams = unflatten_params(flat_target)
@@ -517,6 +520,26 @@ def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_sta
     loss = torch.nn.MSELoss()(values, target.unsqueeze(1))
     loss.backward()
     grad = torch.cat([params[k].grad.reshape(-1) for k, _ in PARAM_ORDER]).clone()
+    return float(loss.item()), grad, values.detach().squeeze(1), target
+
+
+def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma):
+    S, N, _ = s_state.shape
+    params = {k: v.clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
+    tparams = unflatten_params(flat_target)
+    mult = multiplicity_complete(S, N)
+    x = node_features(s_state[..., :2], s_state[..., 2:4])
+    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4])
+    a = actions.reshape(-1).to(torch.long)
+    r = rewards.reshape(-1).to(torch.float32)
+    values = gcn_conv_dense(params, x, mult).reshape(S * N, -1).gather(1, a.unsqueeze(1))
+    with torch.no_grad():
+        next_values = gcn_conv_dense(tparams, xn, mult).reshape(S * N, -1).max(dim=1)[0]
+    target = r + gamma * next_values
+    loss = torch.nn.MSELoss()(values, target.unsqueeze(1))
+    loss.backward()
+    grad = torch.cat([(params[k].grad if params[k].grad is not None else torch.zeros_like(params[k])).reshape(-1)
+                      for k, _ in PARAM_ORDER]).clone()
     return float(loss.item()), grad, values.detach().squeeze(1), target
 
 
@@ -554,13 +577,13 @@ def clip_adam(flat_params, grad, adam_m, adam_v, adam_step: int, lr=1e-3, betas=
 
 def td_step(flat_params, flat_target, adam_m, adam_v, adam_step: int,
             s_state, actions, rewards, s_next_state, gamma=0.99, lr=1e-3,
-            betas=(0.9, 0.999), eps=1e-8, max_norm=1.0, edge_index=None, edge_index_next=None):
+            betas=(0.9, 0.999), eps=1e-8, max_norm=1.0, edge_index=None, edge_index_next=None, conv="gat"):
     """One DQN update (train_gcn_dqn.py:112-137): td_loss_grad + clip_adam.
 
     Returns dict(loss, grad (pre-clip), total_norm, params, m, v, step, values, target).
     """
     loss, grad, values, target = td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_state,
-                                              gamma, edge_index, edge_index_next)
+                                              gamma, edge_index, edge_index_next, conv)
     newp, m, v, total_norm = clip_adam(flat_params, grad, adam_m, adam_v, adam_step, lr, betas, eps, max_norm)
     return dict(loss=loss, grad=grad, total_norm=total_norm, params=newp,
                 m=m, v=v, step=adam_step + 1, values=values, target=target)

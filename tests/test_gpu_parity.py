@@ -199,20 +199,21 @@ def test_gpu_reproduces_recorded_reference_actions(sw, golden_weights, trajector
 
 # ------------------------------------------------------------------ fused acting tick
 @pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
-@pytest.mark.parametrize("N,graph,k", [(8, "complete", 0), (12, "knn", 10), (5, "knn", 5), (20, "complete", 0),
-                                      (29, "knn", 6)])
-def test_act_tick_parity(sw, golden_weights, scen, N, graph, k):
+@pytest.mark.parametrize("N,graph,k,conv", [(8, "complete", 0, "gat"), (12, "knn", 10, "gat"), (5, "knn", 5, "gat"),
+                                           (20, "complete", 0, "gat"), (29, "knn", 6, "gat"),
+                                           (8, "complete", 0, "gcn"), (12, "complete", 0, "gcn"), (7, "knn", 4, "gcn")])
+def test_act_tick_parity(sw, golden_weights, scen, N, graph, k, conv):
     B = 150
     p = _params(golden_weights, scen, 7)
     eng = sw.SwarmEngine(scen, N, B, seed=11, params=p, graph=graph, knn_k=max(k, 1), eps=0.35,
-                         replay_capacity=4 * B)
+                         replay_capacity=4 * B, conv=conv)
     pos, vel = _rand_state(B, N, 21, tight=(N == 5))
     eng.state.copy_(torch.cat([pos, vel], -1).cuda())
     eng.ctrl[0] = 5   # tick
     eng.act(push=True)
     torch.cuda.synchronize()
     ref = O.act_tick(O.unflatten_params(p), pos, vel, SCEN[scen], O.GRAPH_COMPLETE if graph == "complete" else O.GRAPH_KNN,
-                     k, 0.35, 11, 5)
+                     k, 0.35, 11, 5, conv=conv)
     assert_close_rel(eng.q.cpu(), ref.q, 1e-5, "Q")
     clear = _tie_mask(ref.q) | ref.explore[:, None]
     assert ref.explore.any() and (~ref.explore).any()
@@ -257,17 +258,21 @@ def _fill_replay(eng, seed):
     eng.ctrl[1] = 0
 
 
-@pytest.mark.parametrize("scen,N,S,graph,k", [("go_to", 8, 32, "complete", 0), ("obstacle_avoidance", 12, 40, "complete", 0),
-                                                ("go_to", 5, 7, "complete", 0), ("go_to", 8, 256, "complete", 0),
-                                                ("go_to", 20, 9, "complete", 0), ("obstacle_avoidance", 29, 5, "complete", 0),
-                                                ("obstacle_avoidance", 12, 24, "knn", 5), ("go_to", 20, 6, "knn", 10)])
-def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k):
+@pytest.mark.parametrize("scen,N,S,graph,k,conv", [
+    ("go_to", 8, 32, "complete", 0, "gat"), ("obstacle_avoidance", 12, 40, "complete", 0, "gat"),
+    ("go_to", 5, 7, "complete", 0, "gat"), ("go_to", 8, 256, "complete", 0, "gat"),
+    ("go_to", 20, 9, "complete", 0, "gat"), ("obstacle_avoidance", 29, 5, "complete", 0, "gat"),
+    ("obstacle_avoidance", 12, 24, "knn", 5, "gat"), ("go_to", 20, 6, "knn", 10, "gat"),
+    # a13 GCNConv variant (C5's "GCN vs GAT"; parity unpinned: checked against the oracle's autograd only)
+    ("go_to", 8, 64, "complete", 0, "gcn"), ("obstacle_avoidance", 12, 40, "complete", 0, "gcn"),
+    ("obstacle_avoidance", 5, 33, "complete", 0, "gcn"), ("go_to", 20, 9, "complete", 0, "gcn")])
+def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k, conv):
     B = 16
     cap = max(4, -(-S // B))
     p = _params(golden_weights, scen, 5)
     tgt = _params(golden_weights, scen, 6)
     eng = sw.SwarmEngine(scen, N, B, seed=2, params=p, batch=S, replay_capacity=cap * B, update_target_every=1000,
-                         graph=graph, knn_k=max(k, 1))
+                         graph=graph, knn_k=max(k, 1), conv=conv)
     eng.target.copy_(tgt.cuda())
     _fill_replay(eng, S)
     idx = torch.randperm(cap * B, generator=torch.Generator().manual_seed(S))[:S].to(torch.int32)
@@ -282,7 +287,8 @@ def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k):
     if graph == "knn":   # per-graph kNN edge lists (simulator.py:15-24), offset like Batch.from_data_list
         ei = torch.cat([O.knn_edge_index(s[g, :, :2], k) + g * N for g in range(S)], dim=1)
         ein = torch.cat([O.knn_edge_index(s1[g, :, :2], k) + g * N for g in range(S)], dim=1)
-    ref = O.td_step(p, tgt, torch.zeros_like(p), torch.zeros_like(p), 0, s, a, r, s1, edge_index=ei, edge_index_next=ein)
+    ref = O.td_step(p, tgt, torch.zeros_like(p), torch.zeros_like(p), 0, s, a, r, s1, edge_index=ei, edge_index_next=ein,
+                    conv=conv)
     grad = eng.grad.cpu()
     loss = grad[O.N_PARAMS].item() / (S * N)
     assert_close_rel(loss, ref["loss"], 1e-5, "TD loss")
@@ -370,13 +376,14 @@ def test_training_is_bitwise_deterministic(sw, golden_weights):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]) and outs[0][2] == outs[1][2]
 
 
-@pytest.mark.parametrize("scen,N,graph", [("GoTo", 8, "complete"), ("ObstacleAvoidance", 12, "knn")])
-def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph):
+@pytest.mark.parametrize("scen,N,graph,conv", [("GoTo", 8, "complete", "gat"), ("ObstacleAvoidance", 12, "knn", "gat"),
+                                               ("ObstacleAvoidance", 10, "complete", "gcn")])
+def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
     """Fused tick (optimizer step deferred into the next act launch, ping-pong buffers)
     == act + td_grad + grad_reduce + adam_step, bit for bit, incl. target syncs."""
     p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 4)
     kw = dict(seed=21, params=p, batch=48, eps=0.25, graph=graph, knn_k=5, update_target_every=3,
-              replay_capacity=16 * 64)
+              replay_capacity=16 * 64, conv=conv)
     a = sw.SwarmEngine(scen, N, 16, **kw)
     b = sw.SwarmEngine(scen, N, 16, **kw)
     a.reset(0)
