@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--mode", default="train", choices=("train", "act"),
                     help="train: fused training tick (headline); act: acting-only rollout with frozen "
                          "weights, eps 0 (Simulator-shaped, replicas only)")
+    ap.add_argument("--tick", default="fused", choices=("fused", "3"),
+                    help="fused: acting + TD blocks in one launch (swarm_train_tick) where supported; "
+                         "3: act / TD / reduce launches")
     ap.add_argument("--batch", type=int, default=None, help="sampled graphs per update per GPU (default = envs)")
     ap.add_argument("--chunk", type=int, default=20, help="ticks per captured hipGraph")
     ap.add_argument("--no-graph", action="store_true")
@@ -128,8 +131,13 @@ def main():
     eng.reset()
     tick_in_ep = [0]
 
+    fused = eng.fused and args.tick == "fused"
+
     def tick():
-        eng.train_tick(full_out=False)
+        if fused:
+            eng.train_tick(full_out=False)
+        else:
+            eng.train_tick3(full_out=False)
 
     chunk = max(1, math.gcd(args.steps, args.chunk)) if args.steps else 1
     graph = None
@@ -192,28 +200,48 @@ def main():
         if not replicas:
             raise SystemExit(f"rank {rank}: replicas diverged after {args.steps} ticks")
 
-    # ---- per-kernel durations: each kernel of the fused tick as a captured chain of KCHAIN
-    #      back-to-back launches (the same inputs every launch: TD and the slab reduce are pure
-    #      functions of them; the act launch re-applies the same pending step and advances the
-    #      envs), replayed with HIP events recorded on the stream the graph launches on.
-    #      Back-to-back launches are what the rocprofv3 kernel trace of this command times.
+    # ---- per-kernel durations.  Fused tick: KT real eager ticks queued behind a GPU sleep (so
+    #      the launches run back to back, not at Python's pace), HIP events recorded on the
+    #      launch stream around each kernel; the TD graphs of each tick's own slot really wait
+    #      for their acting waves.  3-launch tick: each kernel as a captured chain of KCHAIN
+    #      back-to-back launches (TD and the slab reduce are pure functions of their inputs).
     kt = {}
     if not args.no_kernel_timing:
         stream = torch.cuda.current_stream()
-        kchain = 50
-        for name, fn in (("td_kernel", eng.launch_td), ("act_kernel", eng.launch_train_act),
-                         ("grad_reduce_kernel", eng.launch_grad_reduce)):
-            fn()
-            g = eng.capture(kchain, fn)
-            per = []
-            for _ in range(5):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                g.replay()
-                e1.record(stream)
-                torch.cuda.synchronize()
-                per.append(e0.elapsed_time(e1) * 1e3 / kchain)
-            kt[name] = float(np.median(per))   # microseconds per launch
+        if fused:
+            KT = 60
+            if tick_in_ep[0] + KT > max_steps:
+                eng.reset()
+                tick_in_ep[0] = 0
+            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(KT)]
+            torch.cuda.synchronize()
+            torch.cuda._sleep(20_000_000)
+            for e in ev:
+                e[0].record(stream)
+                eng.launch_tick()
+                e[1].record(stream)
+                eng.launch_reduce_advance()
+                e[2].record(stream)
+            torch.cuda.synchronize()
+            tick_in_ep[0] += KT
+            kt["tick_kernel"] = float(np.median([e[0].elapsed_time(e[1]) * 1e3 for e in ev[5:]]))
+            kt["grad_reduce_kernel"] = float(np.median([e[1].elapsed_time(e[2]) * 1e3 for e in ev[5:]]))
+            assert eng.handoff_errors() == 0, "fused tick: a hand-off wait hit its bound"
+        else:
+            kchain = 50
+            for name, fn in (("td_kernel", eng.launch_td), ("act_kernel", eng.launch_train_act),
+                             ("grad_reduce_kernel", eng.launch_grad_reduce)):
+                fn()
+                g = eng.capture(kchain, fn)
+                per = []
+                for _ in range(5):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    g.replay()
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    per.append(e0.elapsed_time(e1) * 1e3 / kchain)
+                kt[name] = float(np.median(per))   # microseconds per launch
 
     value = B * N * world * args.steps / elapsed
     ms = elapsed / args.steps * 1e3
@@ -222,19 +250,29 @@ def main():
         td_flops_launch = S * N * (2 * gat_fwd_flops(N, d) + td_bwd_flops(N, d))
     else:
         td_flops_launch = S * N * (2 * gcn_fwd_flops(N, d) + gcn_bwd_flops(N, d))
+    # acting half per agent-step: forward + ~300 FLOP of physics; 69 B (state r/w 32 + push 37)
+    act_flops_launch = B * N * ((gat_fwd_flops(N, d) if args.conv == "gat" else gcn_fwd_flops(N, d)) + 300)
     roof = None
     if kt:
-        t_td = kt["td_kernel"] * 1e-6
-        ach = td_flops_launch / t_td / 1e12
+        headline = (scen, N, B, S, args.conv, args.graph) == ("GoTo", 8, 1024, 1024, "gat", "complete")
+        if fused:   # the dominant kernel is the whole fused tick kernel (acting + TD blocks)
+            t_k = kt["tick_kernel"] * 1e-6
+            flops, nbytes = act_flops_launch + td_flops_launch, B * N * 69 + S * N * 37
+            kname, pmcf = "tick_kernel (swarm_train_tick: acting + TD blocks)", "r01_pmc_tick.json"
+        else:
+            t_k = kt["td_kernel"] * 1e-6
+            flops, nbytes = td_flops_launch, S * N * 37
+            kname, pmcf = "td_kernel (swarm_td_grad)", "r01_pmc_td.json"
+        ach = flops / t_k / 1e12
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r01_pmc_td.json")
-        if os.path.exists(pmc) and (scen, N, B, S, args.conv, args.graph) == ("GoTo", 8, 1024, 1024, "gat", "complete"):
+        pmc = os.path.join(ROOT, "profiles", pmcf)
+        if os.path.exists(pmc) and headline:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": "td_kernel (swarm_td_grad)",
-                "algorithmic_flops_per_launch": td_flops_launch,
-                "algorithmic_bytes_per_launch": S * N * 37,
-                "hbm_frac": S * N * 37 / t_td / 1e9 / PEAK_HBM_GBS,
+                "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": kname,
+                "algorithmic_flops_per_launch": flops,
+                "algorithmic_bytes_per_launch": nbytes,
+                "hbm_frac": nbytes / t_k / 1e9 / PEAK_HBM_GBS,
                 "kernel_us": {k: round(v, 2) for k, v in kt.items()}}
 
     cpu = None
@@ -263,7 +301,8 @@ def main():
                                        f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
                            "global_envs": B * world, "td_batch_per_gpu": S, "graph": args.graph, "conv": args.conv,
                            "parallelism": f"env-sharded dp{world}" + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce" if distributed else ""),
-                           "hipgraph": graph is not None, "replicas_identical": replicas},
+                           "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
+                           "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu,
                 "loss": ctrl["loss"]}
         print(json.dumps(line))

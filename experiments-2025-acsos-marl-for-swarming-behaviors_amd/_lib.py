@@ -22,7 +22,9 @@ F_SHARED_RESET, F_RANDOM_OA = 1, 2
 N_PARAMS = 1673
 ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
-          -3: "SWARM_E_NOGPU"}
+          -3: "SWARM_E_NOGPU",
+          -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
+ABI_VERSION = 3
 
 
 class SwarmConfig(ctypes.Structure):
@@ -86,6 +88,13 @@ _PROTOS = {
     "swarm_ctrl_init": (c_int32, [POINTER(SwarmAdamCfg), c_float, c_void_p, c_void_p]),
     "swarm_ctrl_advance": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmReplay), c_void_p, c_void_p]),
     "swarm_host_topk_set": (c_int32, [POINTER(c_float), c_int32, c_int32, POINTER(ctypes.c_uint8)]),
+    "swarm_train_tick_supported": (c_int32, [POINTER(SwarmConfig)]),
+    "swarm_train_tick_workspace_bytes": (c_int64, [POINTER(SwarmConfig)]),
+    "swarm_train_tick": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
+                                   POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "swarm_host_sample_index": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
+    "swarm_host_sample_position": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
 }
 EXPORTED = tuple(_PROTOS)
 
@@ -106,7 +115,7 @@ def load(require_gpu: bool = True):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.swarm_abi_version() != 2:
+        if lib.swarm_abi_version() != ABI_VERSION:
             raise RuntimeError("libswarm_hip ABI mismatch")
         _lib = lib
     return _lib

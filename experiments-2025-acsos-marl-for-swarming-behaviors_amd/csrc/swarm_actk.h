@@ -1,0 +1,384 @@
+// swarm_actk.h — body of the acting kernel (reset-free part of the hot path): one wave per
+// environment; graph -> GCN.forward -> eps-greedy -> env.step -> replay push.  Shared by
+// act_kernel (swarm_act.hip) and the fused training-tick kernel (swarm_tick.hip).
+//
+// Reference call sites replaced (paths relative to the reference checkout):
+//   train_gcn_dqn.py:161-172   graph -> model -> eps-greedy -> env.step -> replay.push
+//   simulator.py:59-93         kNN graph -> argmax -> env.step -> metrics
+//   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:242-321
+#pragma once
+#include "swarm_adam.h"
+#include "swarm_env.h"
+#include "swarm_dl.h"
+
+namespace swarm {
+
+enum { MODE_Q = 0, MODE_TICK = 1, MODE_ROLLOUT = 2, MODE_STEP = 3 };
+
+struct ActArgs {
+  int B, N, scenario, graph, k, conv, env_offset, flags;
+  uint32_t k0, k1;
+  const float* params;
+  const float* x;          // MODE_Q node features [B*N][7]
+  const uint8_t* dense;    // SWARM_GRAPH_DENSE multiplicity
+  const int32_t* actions;  // MODE_STEP actions [B][N]
+  float* state;            // [B][N][4]
+  swarm_replay replay;     // replay.s == nullptr -> no push
+  const swarm_ctrl* ctrl;  // MODE_TICK: tick / eps / write_slot
+  swarm_act_out out;
+  int n_ticks;
+  uint32_t tick0;
+  float eps;
+  int learn;               // MODE_TICK: apply the pending optimizer step first (fused tick)
+  swarm_learner lr;
+  swarm_adam_cfg hp;
+  float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
+  int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
+  uint32_t* ho_flags;      // fused tick: [B] publish stamps (swarm_common.h hand-off), or NULL
+  float* ho_rec;           // fused tick: [B][ho_stride_floats(N)] hand-off records
+};
+
+constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
+
+// One wave per environment in the D layout (swarm_dl.h): lane (c, p) serves agent
+// n = 16 ct + c with row group p.  Block-wide work is only the weight image (LDS),
+// staged from global memory or produced by the fused Adam prologue.
+//
+// The first memory round trip's pointers and the geometry lead the parameter list so that
+// they arrive preloaded in SGPRs (kernarg preload, -amdgpu-kernarg-preload-count): the
+// prologue's loads issue at wave start instead of behind a kernarg-segment fetch.
+// SCEN: compile-time scenario (no speculated OA physics).  SPEC fixes graph and conv at
+// compile time (SPEC_* in swarm_common.h) — e.g. the headline configuration's kernel
+// (complete + GAT) carries no kNN / dense / GCN code; SPEC_RUNTIME reads them from A.
+template <int NS>
+struct ActSmem {
+  WScratch<NS> SW[kActWPB];
+  __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
+  float red[8 * kActWPB + 8];
+};
+
+// vb / nvb: this block's index among the nvb acting blocks of the launch (the fused
+// training-tick kernel runs acting blocks beside TD blocks).
+// HO: fused-tick hand-off publishing (swarm_tick.hip only)
+template <int NS, int MODE, int SCEN, int SPEC, bool HO = false>
+__device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int nvb,
+                                         const swarm_ctrl* __restrict__ ctrl, float* state, const float* grad,
+                                         const float* w_cur, const float* m_cur, const float* v_cur, int B, int N,
+                                         const ActArgs& A) {
+  constexpr int CT = DGeom<NS>::CT;
+  WScratch<NS>* SW = S.SW;
+  float* Pw = S.Pw;
+  float* red = S.red;
+  SWARM_RTSTAMP(30);
+  SWARM_STAMP(0);
+  if (HO) __builtin_amdgcn_s_setprio(3);   // fused tick: acting waves ahead of the TD blocks beside them
+  const int w = threadIdx.x >> 6;
+  const DGeom<NS> d = make_dgeom<NS>(vb * kActWPB + w, B);
+  const int graph = spec_graph<SPEC>(A.graph);
+  const int conv = spec_conv<SPEC>(A.conv);
+  const WView<NS> V = SW[w].view();
+  WSmall<NS>& sm = SW[w].sm;
+  const int c = d.c, p = d.p;
+
+  // prologue: every independent global load in flight at once
+  DFwd<NS> F;
+  float px[CT], py[CT], vx[CT], vy[CT];
+  bool valid[CT];
+  size_t node[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = 16 * ct + c;
+    valid[ct] = d.live && n < N;
+    node[ct] = (size_t)d.gid * N + min(n, N - 1);   // idle lanes alias an in-bounds node, never store
+    px[ct] = py[ct] = vx[ct] = vy[ct] = 0.0f;
+    if (MODE == MODE_Q) {
+      F.x[ct][0] = valid[ct] ? A.x[node[ct] * kFeat + p] : 0.0f;
+      F.x[ct][1] = (valid[ct] && 4 + p < kFeat) ? A.x[node[ct] * kFeat + 4 + p] : 0.0f;
+    } else {
+      const float4 st = *reinterpret_cast<const float4*>(state + node[ct] * 4);
+      if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
+    }
+  }
+  // the whole control block in registers, loaded once and up front (two scalar lines in
+  // flight together instead of dependent loads behind branches)
+  swarm_ctrl cc = {};
+  if (MODE == MODE_TICK) cc = *ctrl;
+  uint32_t tick = A.tick0;
+  float eps = A.eps;
+  uint32_t slot = 0;
+  if (MODE == MODE_TICK) {
+    tick = cc.tick;
+    eps = cc.eps;
+    slot = cc.write_slot;
+  }
+  const uint32_t genv = (uint32_t)(A.env_offset + d.gid);
+  // the first tick's eps-greedy coin only needs ctrl: drawn while the prologue's loads fly
+  const bool explore0 = (MODE != MODE_STEP && MODE != MODE_Q && eps > 0.0f) &&
+                        u01(philox4x32(tick, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
+  // fused tick: is this env's transition in the TD batch drawn from this tick's slot?
+  // (position of graph id slot * B + env in the keyed permutation < batch)
+  bool ho_pub = false;
+  if (MODE == MODE_TICK && HO && d.live) {
+    const uint32_t cap = (uint32_t)A.replay.capacity;
+    const uint32_t filled = cc.filled_slots;
+    const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)B;
+    if (ng >= (uint32_t)A.hp.batch) {
+      const SampleKey sk = sample_key_cached(&cc, ng, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, tick);
+      ho_pub = sample_position(slot * (uint32_t)B + (uint32_t)d.gid, sk) < (uint32_t)A.hp.batch;
+    }
+  }
+  // the late stores' pointers fetched from the kernarg segment now, beside the wait
+  // explore0 already has, and pinned in SGPRs: no kernarg round trip later in the wave
+  float* rp_s = A.replay.s;
+  float* rp_sn = A.replay.s_next;
+  float* rp_r = A.replay.r;
+  uint8_t* rp_a = A.replay.a;
+  float* o_rew = A.out.reward;
+  float* o_avg = A.out.avg_dist;
+  float* o_hits = A.out.hits;
+  int32_t* smp = A.sample_out;
+#if SWARM_PIN
+  asm volatile("" : "+s"(rp_s), "+s"(rp_sn), "+s"(rp_r), "+s"(rp_a), "+s"(o_rew), "+s"(o_avg), "+s"(o_hits), "+s"(smp));
+#endif
+  if (MODE == MODE_TICK && A.learn) {
+    // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
+    static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
+    const int tid = threadIdx.x;
+    AdamRegs R;
+    R.load(grad, w_cur, m_cur, v_cur, tid);
+    const uint32_t pending = cc.trained;
+    const uint32_t tnow = cc.tick;
+    const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;
+    float gn = 0.0f;
+    SWARM_STAMP(20);
+    if (pending) gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, tid, red);
+    store_w_lds(Pw, R, tid);
+    SWARM_STAMP(24);
+    if (vb == 0) {
+      store4(A.lr.w_nxt, R.w, R.wt, tid);
+      store4(A.lr.m_nxt, R.m, R.mt, tid);
+      store4(A.lr.v_nxt, R.v, R.vt, tid);
+      if (pending && (tnow % (uint32_t)A.hp.update_target_every) == 0u) store4(A.lr.target, R.w, R.wt, tid);
+      if (pending && tid == 0 && A.grad_norm_out) *A.grad_norm_out = gn;
+    }
+  } else if (MODE != MODE_STEP) {
+    ParamStage<64 * kActWPB> ps;
+    ps.load(A.params, threadIdx.x);
+    ps.store(Pw, threadIdx.x);
+  }
+  __syncthreads();   // weight image complete
+  const float* P = Pw;
+  SWARM_STAMP(1);
+
+  const int n_ticks = (MODE == MODE_ROLLOUT) ? A.n_ticks : 1;
+  float rew_sum[CT], hits_sum = 0.0f;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) rew_sum[ct] = 0.0f;
+  float* fb = &SW[w].H[0][0];   // pair-force scratch [NS][NS][2] (H/T/R rows are free after the forward)
+  static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
+
+  for (int it = 0; it < n_ticks; ++it) {
+    if (MODE != MODE_Q) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        node_x(px[ct], py[ct], vx[ct], vy[ct], 16 * ct + c, p, F.x[ct]);
+        if (!valid[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
+      }
+    }
+    if (MODE != MODE_STEP) {
+      dl_forward<NS, 8>(P, d, N, graph, A.k, conv, A.dense, V, false, F);
+    } else {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        if (16 * ct + c < NS && p == 0) { sm.px[16 * ct + c] = px[ct]; sm.py[16 * ct + c] = py[ct]; }
+      wave_lds_sync();
+    }
+    if (it == 0) SWARM_STAMP(2);
+
+    if (MODE == MODE_Q) {   // the node's row groups store its Q row (from LDS: no lane-indexed registers)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        if (valid[ct])
+          for (int a = p; a < kActions; a += 4) A.out.q[node[ct] * kActions + a] = sm.Q[16 * ct + c][a];
+      return;
+    }
+
+    // ---- eps-greedy (train_gcn_dqn.py:164-167), one Philox coin per env and tick
+    const uint32_t tk = tick + (uint32_t)it;
+    bool explore = explore0;
+    if (it > 0 && eps > 0.0f) explore = u01(philox4x32(tk, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < eps;
+    int action[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int agent = min(16 * ct + c, N - 1);
+      action[ct] = (MODE == MODE_STEP) ? (valid[ct] ? A.actions[node[ct]] : 0) : argmax9(F.q[ct]);
+      if (explore) {   // the action draw only runs on exploring envs
+        const u32x4 wd = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
+        const int j = agent & 3;
+        const uint32_t word = j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w));
+        action[ct] = uniform_int(word, kActions);
+      }
+    }
+
+    if (it == 0) SWARM_STAMP(5);
+    // ---- env.step (VMAS World.step + scenario reward).  The 4 row groups of an agent
+    //      split its partner pairs (group p: partners p, p + 4, ...), then every lane sums
+    //      the forces in VMAS order: 0 + u, obstacle pair, agent pairs in ascending partner
+    //      index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
+    {   // pair mapping independent of the D layout: 64 / NS lanes per agent (NS = 8: one pair per lane)
+      constexpr int LPN = 64 / NS;
+      const int n = d.lane / LPN;
+      const float pxn = sm.px[n], pyn = sm.py[n];
+#pragma unroll
+      for (int j = 0; j < NS / LPN; ++j) {
+        const int u = d.lane % LPN + LPN * j;
+        float gx = 0.0f, gy = 0.0f;
+        if (u < N && n < N) pair_force(pxn - sm.px[u], pyn - sm.py[u], gx, gy);   // u == n: exactly 0
+        *reinterpret_cast<float2*>(fb + 2 * (n * NS + u)) = make_float2(gx, gy);
+      }
+    }
+    if (it == 0) SWARM_STAMP(6);
+    wave_lds_sync();
+    if (it == 0) SWARM_STAMP(7);
+    StepOut o[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = min(16 * ct + c, NS - 1);
+      float fx = 0.0f + action_level(action[ct] / 3);
+      float fy = 0.0f + action_level(action[ct] % 3);
+      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {
+        float gx, gy;
+        pair_force(px[ct] - kObstX, py[ct] - kObstY, gx, gy);
+        fx = fx + gx; fy = fy + gy;
+      }
+      // every slot read at once, no per-partner branch: slots u >= N hold +0 and fx, fy
+      // (started from +0 or +-1) never become -0, so adding them is exact
+      float2 f[NS];
+#pragma unroll
+      for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + u));
+#pragma unroll
+      for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
+      o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
+      if (16 * ct + c < NS && p == 0) { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }
+    }
+    if (it == 0) SWARM_STAMP(3);
+    wave_lds_sync();
+    float dj[NS], hj[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) { dj[j] = sm.aux[j < N ? j : 0]; hj[j] = sm.aux2[j < N ? j : 0]; }
+    float dsum = dj[0], hsum = hj[0];
+#pragma unroll
+    for (int j = 1; j < NS; ++j)
+      if (j < N) { dsum = dsum + dj[j]; hsum = hsum + hj[j]; }
+    float rg = 0.0f;
+    if (SCEN == SWARM_GOTO) {
+      rg = -dj[0];
+#pragma unroll
+      for (int j = 1; j < NS; ++j)
+        if (j < N) rg = rg + (-dj[j]);   // go_to_position_scenario.py:112-113
+    }
+    if (it == 0) SWARM_STAMP(13);
+    const float avg = dsum / (float)N;
+    if (SCEN == SWARM_GOTO) hsum = 0.0f;
+
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const float rew = (SCEN == SWARM_GOTO) ? rg : oa_reward(o[ct].dgoal, o[ct].dobs);
+      const int n = 16 * ct + c;
+      if (valid[ct]) {   // the node's four row groups share its stores
+        if (MODE == MODE_TICK || MODE == MODE_STEP) {
+          if (MODE == MODE_TICK && A.out.q)
+            for (int a = p; a < kActions; a += 4) A.out.q[node[ct] * kActions + a] = sm.Q[n][a];
+          if (MODE == MODE_TICK && A.out.mult && graph != SWARM_GRAPH_DENSE)
+            for (int u = p; u < N; u += 4)
+              A.out.mult[((size_t)d.gid * N + u) * N + n] = (uint8_t)in_mult<NS>(u, n, N, graph, sm, nullptr, d.gid);
+          if (p == 0) {
+            if (A.out.actions) A.out.actions[node[ct]] = action[ct];
+            if (o_rew) o_rew[node[ct]] = rew;
+            if (n == 0) {
+              if (o_avg) o_avg[d.gid] = avg;
+              if (o_hits) o_hits[d.gid] = hsum;
+            }
+          } else if (MODE == MODE_TICK && rp_s) {
+            const size_t ri = ((size_t)slot * B + d.gid) * N + n;
+            if (p == 1) reinterpret_cast<float4*>(rp_s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+            else if (p == 2) reinterpret_cast<float4*>(rp_sn)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
+            else { rp_r[ri] = rew; rp_a[ri] = (uint8_t)action[ct]; }
+            if (HO && ho_pub) {   // write-through copy for this tick's TD wave (hand-off record)
+              float* rec = A.ho_rec + (size_t)d.gid * ho_stride_floats(N);
+              if (p == 1) {
+                st_sc1(rec + 4 * n, px[ct]); st_sc1(rec + 4 * n + 1, py[ct]);
+                st_sc1(rec + 4 * n + 2, vx[ct]); st_sc1(rec + 4 * n + 3, vy[ct]);
+              } else if (p == 2) {
+                float* r2 = rec + 4 * N + 4 * n;
+                st_sc1(r2, o[ct].px); st_sc1(r2 + 1, o[ct].py); st_sc1(r2 + 2, o[ct].vx); st_sc1(r2 + 3, o[ct].vy);
+              } else {
+                st_sc1(rec + 8 * N + n, rew);
+                st_sc1(rec + 9 * N + n, __int_as_float(action[ct]));
+              }
+            }
+          }
+          if (p == 3 && A.out.obs) {
+            float* ob = A.out.obs + node[ct] * 6;
+            ob[0] = o[ct].px; ob[1] = o[ct].py; ob[2] = o[ct].vx; ob[3] = o[ct].vy; ob[4] = kGoalX; ob[5] = kGoalY;
+          }
+        } else if (p == 0) {  // MODE_ROLLOUT
+          if (A.out.traj_pos) {
+            const size_t ti = ((size_t)it * B + d.gid) * N + n;
+            reinterpret_cast<float2*>(A.out.traj_pos)[ti] = make_float2(o[ct].px, o[ct].py);
+          }
+          if (n == 0) {
+            if (A.out.traj_dist) A.out.traj_dist[(size_t)it * B + d.gid] = avg;
+            if (A.out.traj_hits) A.out.traj_hits[(size_t)it * B + d.gid] = hsum;
+          }
+        }
+      }
+      rew_sum[ct] = rew_sum[ct] + rew;
+      px[ct] = o[ct].px; py[ct] = o[ct].py; vx[ct] = o[ct].vx; vy[ct] = o[ct].vy;
+    }
+    hits_sum = hits_sum + hsum;
+    if (MODE == MODE_TICK && HO && ho_pub) {   // every lane's record stores done, then the flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (d.lane == 0)
+        __hip_atomic_store(A.ho_flags + d.gid, cc.tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      SWARM_RTSTAMP(25);
+    }
+    if (it == 0) SWARM_STAMP(14);
+    if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && c == 0 && p == 0 && d.live) {
+      if (A.out.avg_dist) A.out.avg_dist[d.gid] = avg;
+      if (A.out.hits) A.out.hits[d.gid] = hits_sum;
+    }
+    wave_lds_sync();   // every lane done with this tick's LDS rows before the next tick rewrites them
+  }
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    if (valid[ct] && p == 0) {
+      reinterpret_cast<float4*>(state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+      if (MODE == MODE_ROLLOUT) {
+        if (A.out.reward) A.out.reward[node[ct]] = rew_sum[ct];
+        if (A.out.obs) {
+          float* ob = A.out.obs + node[ct] * 6;
+          ob[0] = px[ct]; ob[1] = py[ct]; ob[2] = vx[ct]; ob[3] = vy[ct]; ob[4] = kGoalX; ob[5] = kGoalY;
+        }
+      }
+    }
+  }
+if (MODE == MODE_TICK && smp) {   // at the end of every wave: nothing waits on it
+    // this tick's TD batch (GraphReplayBuffer.sample, train_gcn_dqn.py:40): the keyed
+    // permutation of swarm_td_grad's in-kernel draw, one index per lane of a wave; the
+    // key comes from ctrl's cache (prepared by the previous reduce launch)
+    const uint32_t cap = (uint32_t)A.replay.capacity;
+    const uint32_t filled = cc.filled_slots;
+    const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)B;
+    if (ng >= (uint32_t)A.hp.batch) {
+      const SampleKey sk = sample_key_cached(&cc, ng, A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u), A.k1, tick);
+      const int nw = nvb * kActWPB;
+      for (int i = vb * kActWPB + w + nw * d.lane; i < A.hp.batch; i += nw * 64)
+        smp[i] = (int32_t)sample_index((uint32_t)i, sk);
+    }
+  }
+  SWARM_STAMP(4);
+  SWARM_RTSTAMP(31);
+}
+
+}  // namespace swarm

@@ -139,6 +139,40 @@ __host__ __device__ inline uint32_t sample_index(uint32_t i, const SampleKey& s)
   do { x = feistel(x, s); } while (x >= s.n);
   return x;
 }
+// inverse round order; position of graph id g in the batch permutation (sample_index^-1):
+// cycle walking backwards lands on the unique i < n with sample_index(i) == g
+__host__ __device__ inline uint32_t feistel_inv(uint32_t y, const SampleKey& s) {
+  const int lo_bits = s.bits / 2, hi_bits = s.bits - lo_bits;
+  const uint32_t lo_mask = (1u << lo_bits) - 1u, hi_mask = (1u << hi_bits) - 1u;
+  uint32_t L = y >> lo_bits, R = y & lo_mask;
+  L ^= mix32(R ^ s.rk[3]) & hi_mask;
+  R ^= mix32(L ^ s.rk[2]) & lo_mask;
+  L ^= mix32(R ^ s.rk[1]) & hi_mask;
+  R ^= mix32(L ^ s.rk[0]) & lo_mask;
+  return (L << lo_bits) | R;
+}
+__host__ __device__ inline uint32_t sample_position(uint32_t g, const SampleKey& s) {
+  uint32_t x = g;
+  do { x = feistel_inv(x, s); } while (x >= s.n);
+  return x;
+}
+
+// ---------------------------------------------------------------- fused-tick hand-off
+// The fused training tick (swarm_tick.hip) runs the acting blocks beside the TD blocks.
+// A TD graph drawn from THIS tick's replay slot is the transition an acting wave is still
+// producing: that wave publishes it into an env-exclusive record (whole 128-B lines, so
+// no other producer shares a line) with write-through sc1 stores, waits for them
+// (vmcnt(0)), then sc1-stores the env's flag = tick + 1; the TD wave polls the flag with
+// sc1 loads and reads the record with sc1 loads only (MI355X_MICROARCH.md, inter-workgroup
+// visibility, "Valid forms", first table row).  Record: s [N][4], s' [N][4], r [N], a [N].
+__host__ __device__ constexpr int ho_stride_floats(int N) { return ((10 * N + 31) / 32) * 32; }
+__device__ inline void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline float ld_sc1(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
 
 // ---------------------------------------------------------------- small math
 __host__ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * kLeakySlope; }

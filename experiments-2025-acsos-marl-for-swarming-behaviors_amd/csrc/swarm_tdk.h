@@ -1,0 +1,543 @@
+// swarm_tdk.h — body of the TD kernel: replay sample, TD loss, hand-written backward
+// through GCN (PyG GATConv + MLP), per-block gradient slabs.  Shared by td_kernel
+// (swarm_td.hip) and the fused training-tick kernel (swarm_tick.hip).
+//
+// Reference: DQNTrainer.train_step_dqn (src/training/train_gcn_dqn.py:112-137),
+// GraphReplayBuffer.sample (:38-45), Adam(lr=1e-3) (:85), target sync (:131-133).
+//
+// Layout (swarm_wpg.h): one wave per sampled graph; a block holds 32 node slots.
+// Backward per graph (online wave, per-node vectors in registers):
+//   dQ[a] = (Q[a]-y) * 2/M                      (MSELoss mean, gather)
+//   dR = W2[a]^T dQ ; dZ = dR * [Z>0] ; dT = W1^T dZ ; dOut = dT * (1 - t^2)
+//   GAT: g_uv = dOut_v.h_u ; de_uv = c_uv (g_uv - sum_w c_wv g_wv) ; dp = de * leaky'(p)
+//        da_dst[v] = sum_u dp_uv ; da_src[u] = sum_v dp_uv ; dh_u = sum_v c_uv dOut_v + da_src att_src + da_dst att_dst
+// Parameter sums over the block's 32 node rows: dW1 = dZ^T T, dW2 = dQ^T R, dW = dh^T X on
+// MFMA (32x32x2 f32, node index as K), vectors by LDS column sums; each block writes one
+// slab [N_PARAMS + 1] (last = sum of squared TD errors) and swarm_grad_reduce sums the
+// slabs in a fixed order (bitwise run-to-run reproducible).
+#pragma once
+#include "swarm_adam.h"
+#include "swarm_dl.h"
+
+namespace swarm {
+
+// One TD block = 32 node slots = GPB = 32 / NS sampled graphs.  Wave w < GPB runs the
+// ONLINE network on graph w (forward on s with activations kept, dQ, backward of the
+// per-node vectors); wave GPB + w runs the TARGET network on s' of graph w
+// (y = r + gamma max_a Q_tgt), then shares the parameter products.  The parameter
+// gradient of the block is a sum over its 32 node rows: MFMA 32x32x2 f32 with the
+// node index as K, jobs spread over the waves, each writing its slice of the slab.
+constexpr int kTdRows = 32;
+
+template <int NS>
+struct TdLds {
+  static constexpr int GPB = kTdRows / NS;
+  float H[kTdRows][kRow];         // online conv1.lin output
+  float T[kTdRows][kRow];         // tanh(conv out)
+  float R[kTdRows][kRow];         // relu(lin1)
+  float dZ[kTdRows][kRow];        // dL/d lin1 pre-activation
+  float dO[kTdRows][kRow];        // dL/d conv out
+  float dH[kTdRows][kRow];        // dL/d h
+  float X[kTdRows][9];            // node features (k < 8)
+  float cm[kTdRows][NS + 1];      // c[target row][source slot]
+  float dp[kTdRows][NS + 1];      // dL/d pre-activation of edge (source -> target row)
+  float y[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];
+  int act[kTdRows];
+  WSmall<NS> on[GPB];             // online waves' per-graph scratch
+  WScratch<NS> tg[GPB];           // target waves' forward scratch
+};
+
+struct TdArgs {
+  int S, B, N, graph, k, conv, env_offset;
+  uint32_t k0, k1;
+  const float* params;
+  const float* target;
+  swarm_replay replay;
+  const swarm_ctrl* ctrl;
+  const int32_t* sample_in;
+  int32_t* sample_out;
+  float* slabs;
+  float gamma;
+  float grad_scale;   // fp32(2 / M_local)
+};
+
+// gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
+// measured against nt (1: td 8.4 vs 8.0 us) and write-through sc1 (2: 9.5 us) stores.
+__device__ inline void slab_st(float* p, float v) {
+#if SWARM_SLAB_ST == 1
+  __builtin_nontemporal_store(v, p);
+#elif SWARM_SLAB_ST == 2
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (sc1)
+#else
+  *p = v;
+#endif
+}
+
+// D[i][j] = sum_node A_img[node][i] * B_img[node][j] over the 32 node rows (MFMA, K = node)
+__device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*Bimg)[kRow], int lane) {
+  f32x16 acc = {};
+  const int h = lane >> 5, c = lane & 31;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(Aimg[2 * s + h][c], Bimg[2 * s + h][c], acc);
+  return acc;
+}
+
+// NS node slots per wave holding NS / GS graphs of GS slots (GS = 8 < NS = 16 packs two
+// N <= 8 graphs into one wave: every MFMA column is a real node, one wave per SIMD).
+// The dependent chain's pointers (batch indices -> replay rows) and the geometry lead the
+// parameter list: preloaded into SGPRs (kernarg preload), the index loads issue at wave start.
+template <int NS>
+struct TdSmem {
+  TdLds<NS> TB;
+  __attribute__((aligned(16))) float Pon[N_LDS_PARAMS];
+  __attribute__((aligned(16))) float Ptg[N_LDS_PARAMS];
+  float red[8 * 4 + 8];   // fused tick: the Adam norm partials
+};
+
+// the TD half of the fused training tick (swarm_tick.hip): weights from the pending
+// optimizer step (recomputed in registers, as every acting block does), batch indices
+// drawn in-kernel, this tick's slot read from the acting waves' hand-off records
+struct TdFused {
+  swarm_learner lr;
+  swarm_adam_cfg hp;
+  const uint32_t* ho_flags;   // [B] publish stamps
+  const float* ho_rec;        // [B][ho_stride_floats(N)]
+  uint32_t* ho_err;           // bounded-wait overruns (0 in a correct run)
+};
+constexpr int kHoSpinLimit = 1 << 18;   // polls (with s_sleep) before a hand-off wait gives up
+
+template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
+__device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
+                                        const float* rs_next, const float* rr, const uint8_t* ra, int S, int B,
+                                        int N, int capacity, const TdArgs& A, const TdFused& X) {
+  constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;   // GPB: online (= target) waves per block
+  constexpr int GPW = NS / GS;                             // graphs per wave
+  constexpr int NT = 128 * GPB;
+  static_assert(!FUSED || NT == kAdamNT, "the fused TD block is one Adam workgroup");
+  TdLds<NS>& TB = L.TB;
+  float* Pon = L.Pon;
+  float* Ptg = L.Ptg;
+  const int wave = threadIdx.x >> 6;
+  const bool online = wave < GPB;
+  const int wi = online ? wave : wave - GPB;
+  const DGeom<NS> d = make_dgeom<NS>(vb * GPB + wi, 1 << 30);   // lane geometry; liveness is per graph
+  const int graph = spec_graph<SPEC>(A.graph);
+  const int conv = spec_conv<SPEC>(A.conv);
+  const int row0 = wi * NS;
+  const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
+  const int lane = d.lane, c = d.c, p = d.p;
+  float* gslab = A.slabs + (size_t)vb * (N_PARAMS + 1);
+  SWARM_RTSTAMP(8);
+  SWARM_STAMP(0);
+
+  // ---- 3-launch tick: this wave's replay indices come from the previous launch, so the
+  //      dependent pair (index -> replay rows) is issued first and the weight staging and
+  //      ctrl reads overlap it.  Indices are clamped into the ring: a skipped tick reads
+  //      valid (unused) rows.  Fused tick: the pending Adam step's operands and ctrl first.
+  AdamRegs R;
+  swarm_ctrl cc = {};
+  if (FUSED) {
+    R.load(X.lr.grad, X.lr.w_cur, X.lr.m_cur, X.lr.v_cur, threadIdx.x);
+    cc = *A.ctrl;
+  }
+  const uint32_t cap = (uint32_t)capacity;
+  const uint32_t ring_graphs = cap * (uint32_t)B;
+  int sid[CT];     // batch index of this lane's graph
+  bool live[CT], nv[CT];
+  int jl[CT];      // local node index inside the graph
+  uint32_t gid[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = 16 * ct + c;
+    const int gi = (GS < NS) ? n / GS : 0;
+    jl[ct] = (GS < NS) ? n % GS : n;
+    sid[ct] = vb * (kTdRows / GS) + wi * GPW + gi;
+    live[ct] = sid[ct] < S && n < NS;
+    nv[ct] = live[ct] && jl[ct] < N;
+    gid[ct] = 0;
+    if (!FUSED && sample_in) gid[ct] = min((uint32_t)sample_in[min(sid[ct], S - 1)], ring_graphs - 1u);
+  }
+  ParamStage<NT> pon, ptg;
+  if (!FUSED) pon.load(A.params, threadIdx.x);
+  ptg.load(A.target, threadIdx.x);   // fused: overridden by the new weights on a sync tick
+  const uint32_t filled = FUSED ? cc.filled_slots : A.ctrl->filled_slots;
+  const uint32_t valid_slots = filled + 1 < cap ? filled + 1 : cap;
+  const uint32_t n_graphs = valid_slots * (uint32_t)B;
+  if (FUSED || !sample_in) {   // GraphReplayBuffer.sample: random.sample -> keyed permutation
+    const uint32_t k0 = A.k0 ^ ((uint32_t)A.env_offset * 0x9E3779B9u);
+    const SampleKey sk = FUSED ? sample_key_cached(&cc, n_graphs, k0, A.k1, cc.tick)
+                               : sample_key(n_graphs, k0, A.k1, A.ctrl->tick);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      gid[ct] = n_graphs >= (uint32_t)S ? sample_index((uint32_t)min(sid[ct], S - 1), sk) : 0u;
+  }
+  // fused: graphs of this tick's slot come from the acting waves' hand-off records
+  bool ho[CT];
+  bool wait = false;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    ho[ct] = FUSED && live[ct] && n_graphs >= (uint32_t)S && gid[ct] / (uint32_t)B == cc.write_slot;
+    wait = wait || ho[ct];
+  }
+  // replay rows written by earlier ticks: loads issued now (fused: every lane but the hand-off ones)
+  float rew[CT];
+  int act[CT];
+  float4 st[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const uint32_t slot = gid[ct] / (uint32_t)B, genv = gid[ct] % (uint32_t)B;
+    const size_t ri = ((size_t)slot * B + genv) * N + min(jl[ct], N - 1);
+    st[ct] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    rew[ct] = 0.0f;
+    act[ct] = 0;
+    if (!ho[ct]) {
+      st[ct] = reinterpret_cast<const float4*>(online ? rs : rs_next)[ri];
+      rew[ct] = rr[ri];
+      act[ct] = nv[ct] ? (int)ra[ri] : 0;
+    }
+  }
+  // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
+  if (n_graphs < (uint32_t)S) {
+    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) slab_st(gslab + (q), 0.0f);
+    return;
+  }
+  if (A.sample_out && online && p == 0) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      if (live[ct] && jl[ct] == 0) A.sample_out[sid[ct]] = (int32_t)gid[ct];
+  }
+  SWARM_STAMP(1);
+  const bool waited = FUSED && __builtin_amdgcn_ballot_w64(wait) != 0;
+  if (FUSED) {   // the pending optimizer step (train_gcn_dqn.py:125-133), as every acting block does;
+                 // done before any hand-off wait so that none of it follows the wait
+    const bool pending = cc.trained != 0u;
+    if (pending) adam_apply(R, X.hp, cc.adam_step_size, cc.adam_inv_bc2, threadIdx.x, L.red);
+    store_w_lds(Pon, R, threadIdx.x);
+    if (pending && (cc.tick % (uint32_t)X.hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
+    else ptg.store(Ptg, threadIdx.x);
+    // waves whose graphs wait for a hand-off are the tick's critical path: top issue priority
+    if (waited) {
+      const uint32_t stamp = cc.tick + 1u;
+      for (int spin = 0;; ++spin) {
+        if (wait) {
+          bool miss = false;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            if (ho[ct])
+              miss = miss || __hip_atomic_load(X.ho_flags + gid[ct] % (uint32_t)B, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) != stamp;
+          wait = miss;
+        }
+        if (!__builtin_amdgcn_ballot_w64(wait)) break;
+        if (spin >= kHoSpinLimit) {   // never in a correct run: count it, read what is there
+          if (lane == 0) atomicAdd(X.ho_err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      asm volatile("" ::: "memory");   // the record loads stay behind the matched poll
+      SWARM_RTSTAMP(10);
+      __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        if (ho[ct]) {
+          const float* rec = X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_floats(N);
+          const int j = min(jl[ct], N - 1);
+          const float* sp = rec + (online ? 0 : 4 * N) + 4 * j;
+          st[ct].x = ld_sc1(sp); st[ct].y = ld_sc1(sp + 1); st[ct].z = ld_sc1(sp + 2); st[ct].w = ld_sc1(sp + 3);
+          rew[ct] = ld_sc1(rec + 8 * N + j);
+          act[ct] = nv[ct] ? __float_as_int(ld_sc1(rec + 9 * N + j)) : 0;
+        }
+      }
+    }
+  }
+  DFwd<NS> F;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    node_x(st[ct].x, st[ct].y, st[ct].z, st[ct].w, jl[ct], p, F.x[ct]);
+    if (!nv[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
+  }
+  if (!FUSED) {
+    pon.store(Pon, threadIdx.x);
+    ptg.store(Ptg, threadIdx.x);
+  }
+  if (online && p == 0) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = act[ct];
+  }
+  __syncthreads();   // B0: weight images
+  SWARM_STAMP(2);
+  // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121).
+  //      Everything after B1 waits for the target waves' y, so they issue first.
+  if (!online && !waited) __builtin_amdgcn_s_setprio(2);
+  dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, conv, nullptr, V, online, F);
+  if (!online && p == 0) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      float qmax = F.q[ct][0];
+#pragma unroll
+      for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[ct][a]);
+      if (16 * ct + c < NS) TB.y[row0 + 16 * ct + c] = nv[ct] ? rew[ct] + A.gamma * qmax : 0.0f;
+    }
+  }
+  if (!online && !waited) __builtin_amdgcn_s_setprio(0);
+  SWARM_STAMP(3);
+  __syncthreads();   // B1: TD targets
+  SWARM_STAMP(4);
+
+  const float* P = Pon;
+  float dz[CT][2][4];
+  if (online) {
+    // ---- dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ, dZ = dR * [z > 0]
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c, nn = min(n, NS - 1);
+      float qa = F.q[ct][0];
+#pragma unroll
+      for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? F.q[ct][a] : qa;
+      const float delta = nv[ct] ? (qa - TB.y[row0 + nn]) : 0.0f;
+      const float gq = delta * A.grad_scale;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float4 w = *reinterpret_cast<const float4*>(P + L_W2 + act[ct] * kWRow + 16 * t + 4 * p);
+        const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz[ct][t][r] = F.zr[ct][t][r] > 0.0f ? wv[r] * gq : 0.0f;
+      }
+      if (n < NS) {
+        const int row = row0 + n;
+        *reinterpret_cast<float4*>(&TB.dZ[row][4 * p]) = make_float4(dz[ct][0][0], dz[ct][0][1], dz[ct][0][2], dz[ct][0][3]);
+        *reinterpret_cast<float4*>(&TB.dZ[row][16 + 4 * p]) = make_float4(dz[ct][1][0], dz[ct][1][1], dz[ct][1][2], dz[ct][1][3]);
+        TB.X[row][p] = F.x[ct][0];
+        TB.X[row][4 + p] = F.x[ct][1];
+#pragma unroll
+        for (int j = 0; j < NS / 4; ++j) TB.cm[row][4 * j + p] = pick4(F.cf[ct], j, p);
+        if (p == 0) { TB.X[row][8] = 0.0f; TB.gq[row] = gq; TB.d2[row] = delta * delta; }
+      }
+    }
+  }
+  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph
+  SWARM_STAMP(5);
+
+  const int col = lane & 31, h = lane >> 5;
+  if (online) {
+    // ---- dT^T = W1^T dZ^T on MFMA (the dz registers are the B operand),
+    //      dO = dT * (1 - t^2) with the forward's tanh registers
+    float dO[CT][2][4];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc = mfma16(P[L_W1 + (16 * t + 4 * p + r) * kWRow + 16 * t2 + c], dz[ct][t][r], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dO[ct][t2][r] = nv[ct] ? acc[r] * (1.0f - F.t[ct][t2][r] * F.t[ct][t2][r]) : 0.0f;
+      }
+      if (n < NS) {
+        *reinterpret_cast<float4*>(&TB.dO[row0 + n][4 * p]) = make_float4(dO[ct][0][0], dO[ct][0][1], dO[ct][0][2], dO[ct][0][3]);
+        *reinterpret_cast<float4*>(&TB.dO[row0 + n][16 + 4 * p]) = make_float4(dO[ct][1][0], dO[ct][1][1], dO[ct][1][2], dO[ct][1][3]);
+      }
+    }
+    SWARM_STAMP(24);
+    // ---- GAT backward (attention part).  g[u][v] = H_u . dO_v on MFMA (A = H rows,
+    //      B = the dO registers); lane (c, p) holds g[u = 16 ut + 4 p + r][v = 16 ct + c]
+    float da_d[CT];
+    WSmall<NS>& sm = *V.sm;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) da_d[ct] = 0.0f;
+    if (conv == SWARM_CONV_GAT) {
+      float ah[CT][2][4];
+#pragma unroll
+      for (int ut = 0; ut < CT; ++ut) {
+        const int u = min(16 * ut + c, NS - 1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float4 hv = *reinterpret_cast<const float4*>(&TB.H[row0 + u][16 * t + 4 * p]);
+          ah[ut][t][0] = hv.x; ah[ut][t][1] = hv.y; ah[ut][t][2] = hv.z; ah[ut][t][3] = hv.w;
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int v = 16 * ct + c;
+        float gv[CT][4], cu[CT][4];
+        float part = 0.0f;
+#pragma unroll
+        for (int ut = 0; ut < CT; ++ut) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc = mfma16(ah[ut][t][r], dO[ct][t][r], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // coefficient of edge u -> v, u = 16 ut + 4 p + r (registers hold every u of target v)
+            float cc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int uq = 16 * ut + 4 * q + r;
+              cc[q] = uq < NS ? F.cf[ct][uq < NS ? uq : 0] : 0.0f;
+            }
+            cu[ut][r] = p == 0 ? cc[0] : (p == 1 ? cc[1] : (p == 2 ? cc[2] : cc[3]));
+            gv[ut][r] = acc[r];
+            part = part + cu[ut][r] * gv[ut][r];
+          }
+        }
+        const float Gs = row4_sum(part);
+        float dsum = 0.0f;
+#pragma unroll
+        for (int ut = 0; ut < CT; ++ut)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = 16 * ut + 4 * p + r;
+            float dpu = 0.0f;
+            if (u < NS && cu[ut][r] != 0.0f && nv[ct]) {   // in-edges only (cross-graph / absent: c = 0)
+              const float de = cu[ut][r] * (gv[ut][r] - Gs);
+              const float pre = sm.ssrc[u] + F.sdst[ct];
+              dpu = pre > 0.0f ? de : de * kLeakySlope;
+            }
+            dsum = dsum + dpu;
+            if (u < NS && v < NS) TB.dp[row0 + v][u] = dpu;
+          }
+        da_d[ct] = row4_sum(dsum);
+      }
+    }
+    wave_lds_sync();   // dp / dO rows of this graph
+    SWARM_STAMP(25);
+    // ---- dh_u = sum_v c[v][u] dO_v (MFMA: A = dO rows, B = C column) + da_src att_src + da_dst att_dst
+    const float4 s0 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 4 * p);
+    const float4 s1 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 16 + 4 * p);
+    const float4 d0 = *reinterpret_cast<const float4*>(P + L_ATT_DST + 4 * p);
+    const float4 d1 = *reinterpret_cast<const float4*>(P + L_ATT_DST + 16 + 4 * p);
+    const float as[2][4] = {{s0.x, s0.y, s0.z, s0.w}, {s1.x, s1.y, s1.z, s1.w}};
+    const float ad[2][4] = {{d0.x, d0.y, d0.z, d0.w}, {d1.x, d1.y, d1.z, d1.w}};
+    float ao[2][NS / 4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < NS / 4; ++ks) ao[t][ks] = TB.dO[row0 + 4 * ks + p][16 * t + c];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int u = 16 * ct + c, uu = min(u, NS - 1);
+      float da_s = 0.0f;
+      if (conv == SWARM_CONV_GAT) {   // sum over the targets v of u's own graph
+        const int base = (GS < NS) ? (uu / GS) * GS : 0;
+#pragma unroll
+        for (int j = 0; j < GS; ++j)
+          if (j < N) da_s = da_s + TB.dp[row0 + base + j][uu];
+      }
+      const float das = nv[ct] ? da_s : 0.0f, dad = nv[ct] ? da_d[ct] : 0.0f;
+      f32x4 m0 = {0.f, 0.f, 0.f, 0.f}, m1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NS / 4; ++ks) {
+        const float b = TB.cm[row0 + 4 * ks + p][uu];
+        m0 = mfma16(ao[0][ks], b, m0);
+        m1 = mfma16(ao[1][ks], b, m1);
+      }
+      float dh[2][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dh[0][r] = nv[ct] ? (m0[r] + das * as[0][r]) + dad * ad[0][r] : 0.0f;
+        dh[1][r] = nv[ct] ? (m1[r] + das * as[1][r]) + dad * ad[1][r] : 0.0f;
+      }
+      if (u < NS) {
+        *reinterpret_cast<float4*>(&TB.dH[row0 + u][4 * p]) = make_float4(dh[0][0], dh[0][1], dh[0][2], dh[0][3]);
+        *reinterpret_cast<float4*>(&TB.dH[row0 + u][16 + 4 * p]) = make_float4(dh[1][0], dh[1][1], dh[1][2], dh[1][3]);
+        if (p == 0) { TB.das[row0 + u] = das; TB.dad[row0 + u] = dad; }
+      }
+    }
+    SWARM_STAMP(27);
+  } else {
+    // ---- target waves: products that need only B2's images
+    //      job 0: dW1 = dZ^T T ; job 1: dW2 = onehot(a) gq R, db2, loss ; job 2: db1
+    for (int job = wi; job < 3; job += GPB) {
+      if (job == 0) {
+        const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) slab_st(gslab + (OFF_W1 + acc_row(r, h) * kHidden + col), dW1[r]);
+      } else if (job == 1) {
+        f32x16 dW2 = {};
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int n = 2 * s + h;
+          const float a = (TB.act[n] == col) ? TB.gq[n] : 0.0f;
+          dW2 = mfma32(a, TB.R[n][col], dW2);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int a = acc_row(r, h);
+          if (a < kActions) slab_st(gslab + (OFF_W2 + a * kHidden + col), dW2[r]);
+        }
+        if (lane < kActions || lane == 63) {   // every read issued before the ordered sum
+          float v[kTdRows];
+#pragma unroll
+          for (int n = 0; n < kTdRows; ++n) v[n] = lane == 63 ? TB.d2[n] : (TB.act[n] == lane ? TB.gq[n] : 0.0f);
+          float acc = v[0];
+#pragma unroll
+          for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+          slab_st(gslab + (lane == 63 ? N_PARAMS : OFF_B2 + lane), acc);
+        }
+      } else {
+        if (lane < kHidden) {
+          float v[kTdRows];
+#pragma unroll
+          for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
+          float acc = v[0];
+#pragma unroll
+          for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+          slab_st(gslab + (OFF_B1 + lane), acc);
+        }
+      }
+    }
+  }
+  __syncthreads();   // B3: dO / dH / das / dad
+  SWARM_STAMP(6);
+  // ---- products over B3's images, spread over all 2 GPB waves of the block:
+  //      job 0 / 1: dW rows 0-15 / 16-31 = sum_n dH[n][f] X[n][k] (MFMA 16x16x4, K = node rows)
+  //      job 2: att_src / att_dst (lane halves) ; job 3: dbias
+  {
+    const int wall = online ? wi : GPB + wi;
+    for (int job = wall; job < 4; job += 2 * GPB) {
+      if (job < 2) {
+        const int t = job;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < kTdRows / 4; ++ks) {
+          const int n = 4 * ks + p;
+          acc = mfma16(TB.dH[n][16 * t + c], c < kFeat ? TB.X[n][c] : 0.0f, acc);
+        }
+        if (c < kFeat) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) slab_st(gslab + (OFF_W + (16 * t + 4 * p + r) * kFeat + c), acc[r]);
+        }
+      } else if (job == 2) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
+        const float* da = h == 0 ? TB.das : TB.dad;
+        float v[kTdRows];
+#pragma unroll
+        for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        slab_st(gslab + ((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col), acc);
+      } else if (lane < kHidden) {
+        float v[kTdRows];
+#pragma unroll
+        for (int n = 0; n < kTdRows; ++n) v[n] = TB.dO[n][lane];
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        slab_st(gslab + (OFF_BIAS + lane), acc);
+      }
+    }
+  }
+  SWARM_STAMP(7);
+  SWARM_RTSTAMP(9);
+}
+
+}  // namespace swarm

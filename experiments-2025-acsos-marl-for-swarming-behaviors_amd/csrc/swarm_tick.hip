@@ -1,0 +1,139 @@
+// swarm_tick.hip — the fused training tick: the acting blocks and the TD blocks of one
+// tick in ONE launch, followed by swarm_reduce_advance (2 launches per tick instead of 3).
+// gfx950 only.
+//
+// Reference: the hot loop of DQNTrainer.train_model (src/training/train_gcn_dqn.py:153-178):
+//   graph -> model -> eps-greedy -> env.step -> replay.push -> train_step_dqn (:112-137).
+//
+// Blocks [0, n_act) are acting blocks (swarm_actk.h, one env per wave); blocks
+// [n_act, n_act + n_td) are TD blocks (swarm_tdk.h).  Both apply the pending optimizer step
+// of the previous tick in registers, so neither waits on a launch boundary for the weights.
+// The only in-launch dependency is the reference's push-then-sample order: a TD graph drawn
+// from THIS tick's replay slot waits for the acting wave of its env, which publishes the
+// transition through the sc1 hand-off record (swarm_common.h).  Acting blocks never wait
+// and have the lower block indices; the wait is bounded (kHoSpinLimit) and counted in the
+// workspace's error word, so the grid always drains.  Every other TD graph (slots written by
+// earlier ticks) runs concurrently with acting.
+#include "swarm_actk.h"
+#include "swarm_tdk.h"
+
+namespace swarm {
+
+template <int NSA, int NST>
+union TickSmem {
+  ActSmem<NSA> a;
+  TdSmem<NST> t;
+};
+
+template <int NSA, int NST, int GS, int SCEN, int SPEC>
+__global__ __launch_bounds__(256) void tick_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
+                                                   const float* grad, const float* w_cur, const float* m_cur,
+                                                   const float* v_cur, int B, int N, int n_act, ActArgs A,
+                                                   TdArgs T, TdFused X) {
+  static_assert(64 * kActWPB == 256 && 128 * (kTdRows / NST) == 256, "one block shape for both halves");
+  __shared__ TickSmem<NSA, NST> U;
+  if ((int)blockIdx.x < n_act)
+    act_body<NSA, MODE_TICK, SCEN, SPEC, true>(U.a, blockIdx.x, n_act, ctrl, state, grad, w_cur, m_cur, v_cur, B, N,
+                                               A);
+  else
+    td_body<NST, GS, SPEC, true>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next, T.replay.r,
+                                 T.replay.a, T.S, B, N, T.replay.capacity, T, X);
+}
+
+}  // namespace swarm
+
+using namespace swarm;
+
+namespace {
+// workspace: [flags: B u32][err: 1 u32] (each rounded to 128 B), then the records
+size_t flags_bytes(int B) { return (((size_t)B * 4 + 127) / 128) * 128; }
+size_t err_bytes() { return 128; }
+size_t rec_bytes(int B, int N) { return (size_t)B * ho_stride_floats(N) * 4; }
+}  // namespace
+
+extern "C" {
+
+int swarm_train_tick_supported(const swarm_config* cfg) {
+  if (!cfg || cfg->n_agents < 1 || cfg->n_agents > 16 || cfg->n_envs < 1) return 0;
+  return cfg->graph == SWARM_GRAPH_COMPLETE && (cfg->conv == SWARM_CONV_GAT || cfg->conv == SWARM_CONV_GCN) &&
+         (cfg->scenario == SWARM_GOTO || cfg->scenario == SWARM_OBSTACLE_AVOIDANCE);
+}
+
+int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg) {
+  if (!swarm_train_tick_supported(cfg)) return SWARM_E_UNSUPPORTED;
+  return (int64_t)(flags_bytes(cfg->n_envs) + err_bytes() + rec_bytes(cfg->n_envs, cfg->n_agents));
+}
+
+int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
+                     const swarm_replay* replay, const swarm_ctrl* ctrl, const swarm_act_out* out, float* slabs,
+                     void* workspace, int32_t* sample_out, void* stream) {
+  if (!cfg || !hp || !lr || !replay || !ctrl || !slabs || !workspace || !state) return SWARM_E_BADARG;
+  if (!swarm_train_tick_supported(cfg)) return SWARM_E_UNSUPPORTED;
+  if (hp->batch < 1 || hp->world_size < 1 || hp->update_target_every < 1 || replay->capacity < 1 || !replay->s)
+    return SWARM_E_BADARG;
+  const int B = cfg->n_envs, N = cfg->n_agents;
+  char* ws = static_cast<char*>(workspace);
+  uint32_t* flags = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* err = reinterpret_cast<uint32_t*>(ws + flags_bytes(B));
+  float* rec = reinterpret_cast<float*>(ws + flags_bytes(B) + err_bytes());
+
+  ActArgs a = {};
+  a.B = B; a.N = N; a.scenario = cfg->scenario; a.graph = cfg->graph; a.k = cfg->knn_k; a.conv = cfg->conv;
+  a.env_offset = cfg->env_offset; a.flags = cfg->flags;
+  a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(cfg->seed >> 32);
+  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = nullptr;
+  a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
+  a.replay = *replay;
+  if (out) a.out = *out;
+  a.ho_flags = flags; a.ho_rec = rec;
+
+  TdArgs t = {};
+  t.S = hp->batch; t.B = B; t.N = N; t.graph = cfg->graph; t.k = cfg->knn_k; t.conv = cfg->conv;
+  t.env_offset = cfg->env_offset; t.k0 = a.k0; t.k1 = a.k1;
+  t.params = lr->w_nxt; t.target = lr->target; t.replay = *replay; t.ctrl = ctrl;
+  t.sample_in = nullptr; t.sample_out = sample_out; t.slabs = slabs;
+  t.gamma = hp->gamma;
+  t.grad_scale = (float)(2.0 / ((double)hp->batch * (double)N));
+
+  TdFused x = {};
+  x.lr = *lr; x.hp = *hp; x.ho_flags = flags; x.ho_rec = rec; x.ho_err = err;
+
+  const int n_act = (B + kActWPB - 1) / kActWPB;
+  const int gs = N <= 8 ? 8 : 16;
+  const int n_td = (hp->batch + (kTdRows / gs) - 1) / (kTdRows / gs);
+  const dim3 grid(n_act + n_td), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  const float *g = lr->grad, *w = lr->w_cur, *m = lr->m_cur, *v = lr->v_cur;
+  const bool oa = cfg->scenario == SWARM_OBSTACLE_AVOIDANCE;
+  const bool gat = cfg->conv == SWARM_CONV_GAT;
+#define SWARM_TICK_LAUNCH(NSA, GS, SC, SP) \
+  hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP>), grid, block, 0, st, ctrl, state, g, w, m, v, B, N, n_act, a, t, x)
+#define SWARM_TICK_LAUNCH2(NSA, GS, SC)                                      \
+  do {                                                                        \
+    if (gat) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GAT);               \
+    else SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GCN);                   \
+  } while (0)
+  if (N <= 8) {
+    if (oa) SWARM_TICK_LAUNCH2(8, 8, SWARM_OBSTACLE_AVOIDANCE);
+    else SWARM_TICK_LAUNCH2(8, 8, SWARM_GOTO);
+  } else {
+    if (oa) SWARM_TICK_LAUNCH2(16, 16, SWARM_OBSTACLE_AVOIDANCE);
+    else SWARM_TICK_LAUNCH2(16, 16, SWARM_GOTO);
+  }
+#undef SWARM_TICK_LAUNCH2
+#undef SWARM_TICK_LAUNCH
+  return (int)hipGetLastError();
+}
+
+#if SWARM_STAMPS
+int swarm_dbg_stamps_tick(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_swarm_stamps), &p, sizeof(p)); }
+#endif
+
+uint32_t swarm_host_sample_index(uint32_t i, uint32_t n, uint32_t k0, uint32_t k1, uint32_t tick) {
+  return sample_index(i, sample_key(n, k0, k1, tick));
+}
+uint32_t swarm_host_sample_position(uint32_t g, uint32_t n, uint32_t k0, uint32_t k1, uint32_t tick) {
+  return sample_position(g, sample_key(n, k0, k1, tick));
+}
+
+}  // extern "C"

@@ -3,12 +3,19 @@ all resident in HBM, driven through libswarm_hip.so.
 
 One fused training tick (the reference's hot loop, src/training/train_gcn_dqn.py:153-178):
 
-    swarm_train_act_step  [clip + Adam of the previous tick's gradient, target sync]
-                          graph -> GAT Q -> eps-greedy -> env.step -> replay push,
-                          this tick's TD batch indices                                (1 launch)
-    swarm_td_grad         batch rows -> target fwd -> online fwd -> TD loss -> backward (1 launch)
+    swarm_train_tick      acting blocks: [clip + Adam of the previous tick's gradient, target
+                          sync] graph -> GAT Q -> eps-greedy -> env.step -> replay push;
+                          TD blocks beside them: [the same optimizer step] batch rows ->
+                          target fwd -> online fwd -> TD loss -> backward              (1 launch)
     swarm_reduce_advance  deterministic slab sum, ping-pong copy-back, ctrl advance    (1 launch)
     [all_reduce(grad) over RCCL when world_size > 1]
+
+TD graphs drawn from the tick's own replay slot (push before sample, as the reference)
+wait in-kernel for the acting wave of their env (write-through hand-off records in
+``tick_ws``).  Configurations without a fused-tick kernel (kNN training graph,
+n_agents > 16) run the 3-launch tick (``train_tick3``: swarm_train_act_step ->
+swarm_td_grad -> swarm_reduce_advance); both are bit-identical to each other and to the
+unfused API sequence.
 
 The optimizer step of tick t runs at the start of tick t+1's acting launch (before any
 use of the weights), so every weight the reference would use is used; ``flush()``
@@ -140,6 +147,14 @@ class SwarmEngine:
         self.grad = torch.zeros(N_PARAMS + 3, **f32)
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
+        # fused-tick workspace (hand-off flags, error word, records); zeroed with ctrl
+        self.fused = learn and bool(self.lib.swarm_train_tick_supported(ctypes_ref(self.cfg)))
+        self.tick_ws = None
+        if self.fused:
+            nb = self.lib.swarm_train_tick_workspace_bytes(ctypes_ref(self.cfg))
+            check(int(min(nb, 0)), "swarm_train_tick_workspace_bytes")
+            self.tick_ws = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
+            self._ho_err_off = -(-4 * n_envs // 128) * 128
         # per-tick outputs
         self.q = torch.zeros(n_envs, n_agents, 9, **f32)
         self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
@@ -253,9 +268,35 @@ class SwarmEngine:
         check(self.lib.swarm_grad_reduce(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
+    def launch_tick(self, full_out: bool = False):
+        check(self.lib.swarm_train_tick(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
+                                        ptr(self.state), ctypes_ref(self.replay), ptr(self.ctrl),
+                                        ctypes_ref(self.out if full_out else self.out_min), ptr(self.slabs),
+                                        ptr(self.tick_ws), ptr(self.samples), stream_ptr()), "swarm_train_tick")
+
+    def launch_reduce_advance(self):
+        check(self.lib.swarm_reduce_advance(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
+                                            ctypes_ref(self.learner), self.capacity, ptr(self.ctrl), stream_ptr()),
+              "swarm_reduce_advance")
+
+    def handoff_errors(self) -> int:
+        """Hand-off waits of the fused tick that hit their bound (0 in a correct run)."""
+        if self.tick_ws is None:
+            return 0
+        return int(self.tick_ws[self._ho_err_off:self._ho_err_off + 4].view(torch.int32).item())
+
     def train_tick(self, full_out: bool = False):
-        """Fused training tick: 3 launches (+ an RCCL all-reduce when world_size > 1).
-        The act launch also draws this tick's TD batch indices (self.samples)."""
+        """Fused training tick: 2 launches (+ an RCCL all-reduce when world_size > 1), or the
+        3-launch tick where no fused-tick kernel exists.  Writes this tick's TD batch
+        indices to self.samples."""
+        if not self.fused:
+            return self.train_tick3(full_out)
+        self.launch_tick(full_out)
+        self.launch_reduce_advance()
+        self.allreduce_grad()
+
+    def train_tick3(self, full_out: bool = False):
+        """3-launch training tick: act (+ this tick's TD batch indices), TD, reduce."""
         cfg, hp = ctypes_ref(self.cfg), ctypes_ref(self.hp)
         check(self.lib.swarm_train_act_step(cfg, hp, ctypes_ref(self.learner), ptr(self.state),
                                             ctypes_ref(self.replay), ptr(self.ctrl),

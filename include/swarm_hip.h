@@ -22,11 +22,12 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 2
+#define SWARM_ABI_VERSION 3
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
 #define SWARM_E_NOGPU (-3)
+#define SWARM_E_UNSUPPORTED (-4) /* configuration has no fused-tick kernel (use the 3-launch tick) */
 
 enum swarm_scenario { SWARM_GOTO = 0, SWARM_OBSTACLE_AVOIDANCE = 1 };
 enum swarm_graph { SWARM_GRAPH_COMPLETE = 0, SWARM_GRAPH_KNN = 1, SWARM_GRAPH_DENSE = 2 };
@@ -176,6 +177,25 @@ int swarm_act_step(const swarm_config* cfg, const float* params, float* state,
 int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr,
                          float* state, const swarm_replay* replay, const swarm_ctrl* ctrl,
                          const swarm_act_out* out, int32_t* sample_out, void* stream);
+
+/* Fused training tick in ONE launch (train_gcn_dqn.py:153-178 without the optimizer's
+ * launch): acting blocks (as swarm_train_act_step) and TD blocks (as swarm_td_grad with
+ * in-kernel sampling) run side by side; both apply the pending optimizer step in registers.
+ * TD graphs drawn from this tick's replay slot (the reference pushes before it samples,
+ * :170-172) read the acting waves' write-through hand-off records in `workspace`
+ * (swarm_train_tick_workspace_bytes; zero it whenever ctrl is (re)initialised).  Follow with
+ * swarm_reduce_advance [-> all-reduce(grad)].  Bit-identical to the 3-launch sequence.
+ * Complete training graph, GAT or GCNConv, n_agents <= 16; else SWARM_E_UNSUPPORTED. */
+int swarm_train_tick_supported(const swarm_config* cfg);
+int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg);
+int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
+                     const swarm_replay* replay, const swarm_ctrl* ctrl, const swarm_act_out* out,
+                     float* slabs, void* workspace, int32_t* sample_out, void* stream);
+
+/* Host reference of the replay-batch permutation (GraphReplayBuffer.sample restated as a
+ * keyed Feistel permutation; tests): index = batch position -> graph id, and its inverse. */
+uint32_t swarm_host_sample_index(uint32_t i, uint32_t n, uint32_t k0, uint32_t k1, uint32_t tick);
+uint32_t swarm_host_sample_position(uint32_t g, uint32_t n, uint32_t k0, uint32_t k1, uint32_t tick);
 
 /* Slab sum -> lr->grad, copy *_nxt -> *_cur, record the pending update and
  * advance ctrl (tick, replay slot, the next step's Adam scalars). */

@@ -26,13 +26,13 @@ def _host_lib():
 def test_library_exports_every_header_symbol():
     L, lib = _host_lib()
     hdr = open(os.path.join(ROOT, "include", "swarm_hip.h")).read()
-    names = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(swarm_\w+)\(", hdr, re.M))
+    names = set(re.findall(r"^\s*(?:int|int64_t|uint32_t|const char\*)\s+(swarm_\w+)\(", hdr, re.M))
     assert len(names) >= 15
     raw = ctypes.CDLL(L.LIB_PATH)
     for n in sorted(names):
         assert hasattr(raw, n), n
     assert names == set(L.EXPORTED)
-    assert lib.swarm_abi_version() == 2 and lib.swarm_n_params() == O.N_PARAMS
+    assert lib.swarm_abi_version() == 3 and lib.swarm_n_params() == O.N_PARAMS
 
 
 def test_topk_emulation_matches_torch_fixture():
@@ -81,6 +81,20 @@ def test_sample_index_is_a_permutation():
     for n in (1, 2, 3, 7, 64, 100, 1000):
         got = sorted(O.sample_index(i, n, seed=5, rnd=3) for i in range(n))
         assert got == list(range(n))
+
+
+def test_host_sample_permutation_and_inverse_match_oracle():
+    """The keyed batch permutation the kernels draw (swarm_common.h sample_index) matches the
+    oracle's restatement, and sample_position — which the fused tick's acting waves use to
+    decide whether their env's transition is in this tick's TD batch — is its inverse."""
+    L, lib = _host_lib()
+    for n, seed, rnd in ((1, 0, 0), (7, 5, 3), (1024, 0, 101), (1000, 3, 7), (8192 * 3 + 5, 11, 200)):
+        k0, k1 = (int(x) for x in philox.seed_key(seed))
+        idx = [lib.swarm_host_sample_index(i, n, k0, k1, rnd) for i in range(min(n, 300))]
+        assert idx == [O.sample_index(i, n, seed=seed, rnd=rnd) for i in range(min(n, 300))]
+        assert [lib.swarm_host_sample_position(g, n, k0, k1, rnd) for g in idx] == list(range(len(idx)))
+        if n <= 1024:
+            assert sorted(lib.swarm_host_sample_position(g, n, k0, k1, rnd) for g in range(n)) == list(range(n))
 
 
 @pytest.mark.parametrize("n", [1, 5, 8, 12])

@@ -400,6 +400,43 @@ def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
     assert torch.equal(a.state, b.state) and torch.equal(a.rep_s, b.rep_s)
 
 
+@pytest.mark.parametrize("scen,N,conv,B,slots", [("GoTo", 8, "gat", 64, 4), ("GoTo", 5, "gat", 96, 1),
+                                                  ("ObstacleAvoidance", 12, "gat", 64, 3),
+                                                  ("ObstacleAvoidance", 16, "gcn", 40, 2),
+                                                  ("GoTo", 8, "gcn", 1024, 977)])
+def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, conv, B, slots):
+    """swarm_train_tick (acting and TD blocks in one launch, TD graphs of the tick's own slot
+    read through the hand-off records) == the 3-launch tick, bit for bit, every tick.  Small
+    rings make most draws come from the slot being written (slots = 1: all of them)."""
+    p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 2)
+    kw = dict(seed=9, params=p, batch=B, eps=0.3, update_target_every=3, replay_capacity=slots * B, conv=conv)
+    a = sw.SwarmEngine(scen, N, B, **kw)
+    b = sw.SwarmEngine(scen, N, B, **kw)
+    assert a.fused
+    a.reset(0)
+    b.reset(0)
+    n_cur = 0
+    for t in range(8):
+        a.train_tick(full_out=True)
+        b.train_tick3(full_out=True)
+        torch.cuda.synchronize()
+        ca, cb = a.read_ctrl(), b.read_ctrl()
+        assert ca == cb, t
+        if ca["tick"] * B >= B and ca["filled_slots"] * B >= B:
+            assert torch.equal(a.samples, b.samples), t
+            n_cur += int(((a.samples // B) == (ca["write_slot"] - 1) % slots).sum())
+        assert torch.equal(a.grad, b.grad), t
+        assert torch.equal(a.q, b.q) and torch.equal(a.actions, b.actions) and torch.equal(a.reward, b.reward), t
+    a.flush()
+    b.flush()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params) and torch.equal(a.target, b.target)
+    assert torch.equal(a.adam_m, b.adam_m) and torch.equal(a.adam_v, b.adam_v)
+    assert torch.equal(a.state, b.state) and torch.equal(a.rep_s1, b.rep_s1) and torch.equal(a.rep_a, b.rep_a)
+    assert a.handoff_errors() == 0
+    assert slots > 100 or n_cur > 0   # the hand-off path really ran
+
+
 def test_graph_capture_replay_equals_eager(sw, golden_weights):
     p = _params(golden_weights, "go_to", 1)
     a = sw.SwarmEngine("GoTo", 8, 128, seed=8, params=p, batch=128, eps=0.1)

@@ -1,0 +1,66 @@
+"""Diagnostic: timeline of ONE fused training tick (swarm_train_tick) from in-kernel
+s_memrealtime stamps (100 MHz, chip-wide) of the stamps build (libswarm_hip_stamps.so):
+when the acting waves end, when the TD waves whose graphs come from the tick's own replay
+slot get their hand-off, when the TD waves end.  Times in us from the first wave's entry."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["SWARM_LIB_PATH"] = os.path.join(ROOT, "experiments-2025-acsos-marl-for-swarming-behaviors_amd",
+                                            "libswarm_hip_stamps.so")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import swarm_amd  # noqa: E402
+from swarm_amd import _lib  # noqa: E402
+
+
+def main():
+    from swarm_amd import build as swbuild
+    swbuild.build(stamps=True)
+    lib = _lib.load()
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))["weights_go_to"][0])
+    eng = swarm_amd.SwarmEngine("GoTo", N, B, seed=0, params=w0, batch=B, eps=0.05)
+    eng.reset()
+    for _ in range(100):
+        eng.act(push=True, full_out=False)
+        eng.advance()
+    eng.reset()
+    for _ in range(5):
+        eng.train_tick()
+    n_act = (B + 3) // 4
+    n_blocks = n_act + (B + 3) // 4 if N <= 8 else n_act + (B + 1) // 2
+    buf = torch.zeros(n_blocks * 16 * 32, dtype=torch.int64, device="cuda")
+    raw.swarm_dbg_stamps_tick(ctypes.c_void_p(buf.data_ptr()))
+    for rep in range(3):
+        buf.zero_()
+        eng.train_tick()
+        torch.cuda.synchronize()
+        a = buf.cpu().numpy().reshape(n_blocks, 16, 32)
+        act = a[:n_act, :4]
+        td = a[n_act:, :4]
+        t0 = min(act[..., 30][act[..., 30] > 0].min(), td[..., 8][td[..., 8] > 0].min())
+        us = lambda x: (x - t0) / 100.0  # noqa: E731
+        ae = us(act[..., 31][act[..., 31] > 0])
+        te = us(td[..., 9][td[..., 9] > 0])
+        ts = us(td[..., 8][td[..., 8] > 0])
+        pub = us(act[..., 25][act[..., 25] > 0])
+        ho = td[..., 10]
+        blocks_waiting = np.where((ho > 0).any(axis=1))[0]
+        print(f"tick {rep}: act waves end median {np.median(ae):.2f} max {ae.max():.2f} us; "
+              f"TD waves start median {np.median(ts):.2f}, end median {np.median(te):.2f} max {te.max():.2f} us")
+        print(f"  {len(pub)} acting waves published (at {np.sort(pub).round(2).tolist()[:12]} us)")
+        for b in blocks_waiting[:12]:
+            hw = us(ho[b][ho[b] > 0])
+            print(f"  TD block {b}: hand-off at {hw.round(2).tolist()} us, block end {us(td[b, :, 9].max()):.2f} us")
+        nw = te[te > np.percentile(te, 99)]
+        print(f"  slowest 1% TD waves end at {np.sort(nw).round(2).tolist()[-6:]} us")
+
+
+if __name__ == "__main__":
+    main()
