@@ -200,51 +200,49 @@ def main():
         if not replicas:
             raise SystemExit(f"rank {rank}: replicas diverged after {args.steps} ticks")
 
-    # ---- per-kernel durations.  Fused tick: KT real eager ticks queued behind a GPU sleep (so
-    #      the launches run back to back, not at Python's pace), HIP events recorded on the
-    #      launch stream around each kernel; the TD graphs of each tick's own slot really wait
-    #      for their acting waves.  3-launch tick: each kernel as a captured chain of KCHAIN
-    #      back-to-back launches (TD and the slab reduce are pure functions of their inputs).
+    value = B * N * world * args.steps / elapsed
+    ms = elapsed / args.steps * 1e3
+
+    # ---- per-kernel durations.  Fused tick: a captured chain of KCHAIN real tick launches, each
+    #      followed by swarm_ctrl_advance (tick counter, replay slot: every launch publishes and
+    #      waits on fresh hand-off stamps, as in the timed ticks), HIP events recorded on the
+    #      stream the graph launches on; the advance launch's own duration (a chain of it alone)
+    #      is subtracted.  The slab reduce's share of a tick is the tick time minus that.
+    #      3-launch tick: each kernel as a captured chain of KCHAIN back-to-back launches (TD
+    #      and the slab reduce are pure functions of their inputs).
     kt = {}
     if not args.no_kernel_timing:
         stream = torch.cuda.current_stream()
+
+        def chain_us(fn, kchain=50):
+            fn()
+            g = eng.capture(kchain, fn)
+            per = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                g.replay()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                per.append(e0.elapsed_time(e1) * 1e3 / kchain)
+            return float(np.median(per))   # microseconds per launch
+
         if fused:
-            KT = 60
-            if tick_in_ep[0] + KT > max_steps:
-                eng.reset()
-                tick_in_ep[0] = 0
-            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(KT)]
-            torch.cuda.synchronize()
-            torch.cuda._sleep(20_000_000)
-            for e in ev:
-                e[0].record(stream)
-                eng.launch_tick()
-                e[1].record(stream)
-                eng.launch_reduce_advance()
-                e[2].record(stream)
-            torch.cuda.synchronize()
-            tick_in_ep[0] += KT
-            kt["tick_kernel"] = float(np.median([e[0].elapsed_time(e[1]) * 1e3 for e in ev[5:]]))
-            kt["grad_reduce_kernel"] = float(np.median([e[1].elapsed_time(e[2]) * 1e3 for e in ev[5:]]))
+            eng.reset()
+            t_pair = chain_us(lambda: (eng.launch_tick(), eng.advance()), 40)
+            t_adv = chain_us(eng.advance, 40)
+            eng.flush()
+            eng.reset()
+            tick_in_ep[0] = 0
+            kt["tick_kernel"] = t_pair - t_adv
+            kt["ctrl_advance_kernel"] = t_adv
+            kt["grad_reduce_kernel (tick share)"] = ms * 1e3 - kt["tick_kernel"]
             assert eng.handoff_errors() == 0, "fused tick: a hand-off wait hit its bound"
         else:
-            kchain = 50
             for name, fn in (("td_kernel", eng.launch_td), ("act_kernel", eng.launch_train_act),
                              ("grad_reduce_kernel", eng.launch_grad_reduce)):
-                fn()
-                g = eng.capture(kchain, fn)
-                per = []
-                for _ in range(5):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(stream)
-                    g.replay()
-                    e1.record(stream)
-                    torch.cuda.synchronize()
-                    per.append(e0.elapsed_time(e1) * 1e3 / kchain)
-                kt[name] = float(np.median(per))   # microseconds per launch
+                kt[name] = chain_us(fn)
 
-    value = B * N * world * args.steps / elapsed
-    ms = elapsed / args.steps * 1e3
     d = complete_in_degree(N) if args.graph == "complete" else (2 * N * args.knn_k + 1) / N
     if args.conv == "gat":
         td_flops_launch = S * N * (2 * gat_fwd_flops(N, d) + td_bwd_flops(N, d))

@@ -37,25 +37,76 @@ struct ReduceArgs {
   uint32_t k0, k1;        // replay-sampling key (seed ^ rank salt)
 };
 
-// 1024 threads = 16 columns x 64 slab groups (105 blocks: the 1.7 MB of freshly written
-// slabs is read by many CUs at once, 16 KB each); group g sums a contiguous run of slabs
-// with every load issued before the ordered adds, then the 64 group sums of a column are
-// added in group order (fixed order -> bitwise reproducible run to run).
+// 1024 threads = 16 columns x 64 slab groups (105 column blocks: the 1.7 MB of freshly
+// written slabs is read by many CUs at once, 16 KB each); group g sums a contiguous run of
+// slabs with every load issued before the ordered adds, then the 64 group sums of a column
+// are added in a fixed two-level order (8 runs of 8, then the 8 run sums): bitwise
+// reproducible run to run.  Advance mode adds one control block (the last): it prepares
+// and stores the whole ctrl update (Adam scalars of the next step in double, the next
+// tick's sampling key) in parallel with the column blocks, so no column block waits on it.
 constexpr int kRedCols = 16;
 constexpr int kRedGroups = 64;
+constexpr int kRedColBlocks = (N_PARAMS + 1 + kRedCols - 1) / kRedCols;
 // slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start
 __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(const float* slabs, swarm_ctrl* ctrl,
                                                                             int n_slabs, int advance, ReduceArgs A) {
   __shared__ float part[kRedGroups][kRedCols];
+  __shared__ float part2[8][kRedCols];
   SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
+  swarm_ctrl* C = ctrl;
+  if ((int)blockIdx.x == kRedColBlocks) {   // advance mode: the control block
+    // thread 0 advances the counters and the Adam scalars; thread 64 (another wave) derives
+    // the next tick's sampling key; both read ctrl before the barrier, write after it
+    const int t = threadIdx.x;
+    uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
+    double b1p = 1.0, b2p = 1.0;
+    float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
+    SampleKey nk = {};
+    uint32_t nk_n = 0, nk_tick = 0;
+    const uint32_t cap = (uint32_t)A.capacity;
+    if (t == 0) {
+      c_trained = C->trained; c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
+      b1p = ctrl_get_double(C, CTRL_B1POW);
+      b2p = ctrl_get_double(C, CTRL_B2POW);
+      if (c_trained) {   // the step this tick's act kernel applied
+        b1p = b1p * (double)A.hp.beta1;
+        b2p = b2p * (double)A.hp.beta2;
+        adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
+      }
+    } else if (t == 64) {
+      const uint32_t filled = C->filled_slots;
+      const uint32_t f1 = filled + 1 < cap ? filled + 1 : cap;   // filled after this tick
+      nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;       // graphs the next tick samples from
+      nk_tick = C->tick + 1;
+      nk = sample_key(nk_n, A.k0, A.k1, nk_tick);
+    }
+    __syncthreads();
+    if (t == 0) {   // record the pending update, advance the tick
+      const uint32_t valid_slots = c_filled + 1 < cap ? c_filled + 1 : cap;
+      const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
+      if (c_trained) {
+        C->adam_step = c_step + 1;
+        ctrl_set_double(C, CTRL_B1POW, b1p);
+        ctrl_set_double(C, CTRL_B2POW, b2p);
+        C->adam_step_size = next_step_size;
+        C->adam_inv_bc2 = next_inv_bc2;
+      }
+      C->trained = trained;
+      C->tick = c_tick + 1;
+      C->write_slot = (c_slot + 1) % cap;
+      C->filled_slots = valid_slots;
+    } else if (t == 64) {
+      C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
+      C->sample_bits = (uint32_t)nk.bits;
+      C->sample_n = nk_n;
+      C->sample_tick = nk_tick;
+    }
+    return;
+  }
   const int c = threadIdx.x % kRedCols;
   const int col = blockIdx.x * kRedCols + c;
   const int q = threadIdx.x / kRedCols;
-  // advance mode: the thread owning column N_PARAMS is the control block's single writer.
-  // It reads ctrl and prepares the whole update (incl. the double-precision Adam scalars
-  // of the next step) before the slab loads return, and stores it at the end.
-  const bool writer = advance && col == N_PARAMS && q == 0;
   const int per = (n_slabs + kRedGroups - 1) / kRedGroups;
   const int b0 = q * per, b1 = min(n_slabs, b0 + per);
   // first chunk of this thread's slab column in flight before anything else
@@ -64,35 +115,6 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
     v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[(size_t)(b0 + j) * (N_PARAMS + 1) + col] : 0.0f;
-  // advance mode: the thread owning column N_PARAMS is the control block's single writer.
-  // It prepares the whole update (incl. the double-precision Adam scalars of the next
-  // step and the next tick's sampling key) while the slab loads fly, stores it at the end.
-  swarm_ctrl* C = ctrl;
-  uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
-  double b1p = 1.0, b2p = 1.0;
-  float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
-  SampleKey nk = {};
-  uint32_t nk_n = 0, nk_tick = 0;
-  if (writer) {
-    c_trained = C->trained; c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
-    b1p = ctrl_get_double(C, CTRL_B1POW);
-    b2p = ctrl_get_double(C, CTRL_B2POW);
-    if (c_trained) {   // the step this tick's act kernel applied
-      b1p = b1p * (double)A.hp.beta1;
-      b2p = b2p * (double)A.hp.beta2;
-      adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
-    }
-  }
-  // a second wave of the same block prepares the next tick's sampling key in parallel
-  const bool key_writer = advance && col == N_PARAMS && q == 4;
-  if (key_writer) {
-    const uint32_t cap = (uint32_t)A.capacity;
-    const uint32_t filled = C->filled_slots;
-    const uint32_t f1 = filled + 1 < cap ? filled + 1 : cap;   // filled after this tick
-    nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;       // graphs the next tick samples from
-    nk_tick = C->tick + 1;
-    nk = sample_key(nk_n, A.k0, A.k1, nk_tick);
-  }
   float s = v0[0];
 #pragma unroll
   for (int j = 1; j < kChunk; ++j) s = s + v0[j];
@@ -114,34 +136,20 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   part[q][c] = s;
   __syncthreads();
   SWARM_STAMP(30);
-  if (q == 0 && col <= N_PARAMS) {
-    float tot = part[0][c];
+  if (q < 8) {
+    float r = part[8 * q][c];
 #pragma unroll
-    for (int gi = 1; gi < kRedGroups; ++gi) tot = tot + part[gi][c];
-    A.grad[col] = tot;
-    if (writer) {   // record the pending update, advance the tick
-      const uint32_t cap = (uint32_t)A.capacity;
-      const uint32_t valid_slots = c_filled + 1 < cap ? c_filled + 1 : cap;
-      const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
-      if (c_trained) {
-        C->adam_step = c_step + 1;
-        ctrl_set_double(C, CTRL_B1POW, b1p);
-        ctrl_set_double(C, CTRL_B2POW, b2p);
-        C->adam_step_size = next_step_size;
-        C->adam_inv_bc2 = next_inv_bc2;
-      }
-      C->trained = trained;
-      C->loss = trained ? tot / (float)((size_t)A.batch * A.N) : 0.0f;
-      C->tick = c_tick + 1;
-      C->write_slot = (c_slot + 1) % cap;
-      C->filled_slots = valid_slots;
-    }
+    for (int gi = 1; gi < 8; ++gi) r = r + part[8 * q + gi][c];
+    part2[q][c] = r;
   }
-  if (key_writer) {   // after the barrier: every thread of the block has read ctrl
-    C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
-    C->sample_bits = (uint32_t)nk.bits;
-    C->sample_n = nk_n;
-    C->sample_tick = nk_tick;
+  __syncthreads();
+  if (q == 0 && col <= N_PARAMS) {
+    float tot = part2[0][c];
+#pragma unroll
+    for (int gi = 1; gi < 8; ++gi) tot = tot + part2[gi][c];
+    A.grad[col] = tot;
+    // loss of this update (0 when skipped: the TD launch wrote zero slabs)
+    if (advance && col == N_PARAMS) C->loss = tot / (float)((size_t)A.batch * A.N);
   }
   SWARM_STAMP(31);
   SWARM_RTSTAMP(23);
@@ -297,7 +305,7 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
   if (int e = check_td(cfg, hp)) return e;
   ReduceArgs a = {};
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = grad;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + kRedCols - 1) / kRedCols), dim3(kRedCols * kRedGroups), 0,
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(kRedColBlocks), dim3(kRedCols * kRedGroups), 0,
                      (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }
@@ -313,7 +321,7 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   a.hp = *hp;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((N_PARAMS + 1 + kRedCols - 1) / kRedCols), dim3(kRedCols * kRedGroups), 0,
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(kRedColBlocks + 1), dim3(kRedCols * kRedGroups), 0,
                      (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }

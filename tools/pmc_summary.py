@@ -5,7 +5,7 @@ FETCH_SIZE / WRITE_SIZE are in KB per dispatch; on gfx950 FETCH_SIZE reports hal
 bytes of a wide coalesced read, so it is doubled (MI355X_MICROARCH.md §HBM).  Both count
 Infinity-Cache hits, so the figure is fabric traffic below L2, an upper bound on HBM.
 
-usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc_td.json
+usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc_tick.json
 """
 import collections
 import csv
@@ -15,7 +15,7 @@ import os
 import statistics
 import sys
 
-KERNELS = {"td": "td_kernel", "act": "act_kernel<8, 1>", "reduce": "grad_reduce_kernel"}
+KERNELS = {"tick": "tick_kernel", "td": "td_kernel", "act": "act_kernel<8, 1>", "reduce": "grad_reduce_kernel"}
 
 
 def main(src, dst):
@@ -43,8 +43,10 @@ def main(src, dst):
             "per_wave": {c: k[c] / waves for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA",
                                                     "SQ_WAVE_CYCLES", "SQ_WAIT_ANY") if c in k},
         }
-    if "td" in out["kernels"]:
-        out["hbm_bytes_per_launch"] = out["kernels"]["td"]["hbm_bytes_per_launch"]
+    main_k = "tick" if "tick" in out["kernels"] else "td"   # the bench line's dominant kernel
+    if main_k in out["kernels"]:
+        out["kernel"] = main_k
+        out["hbm_bytes_per_launch"] = out["kernels"][main_k]["hbm_bytes_per_launch"]
     json.dump(out, open(dst, "w"), indent=1)
     for key, v in out["kernels"].items():
         print(f"{key:7s} fetch {v['fetch_bytes_corrected'] / 1e3:8.1f} KB  write {v['write_bytes'] / 1e3:8.1f} KB  "
