@@ -34,8 +34,7 @@ struct ActArgs {
   swarm_adam_cfg hp;
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
   int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
-  uint32_t* ho_flags;      // fused tick: [B] publish stamps (swarm_common.h hand-off), or NULL
-  float* ho_rec;           // fused tick: [B][ho_stride_floats(N)] hand-off records
+  unsigned long long* ho_rec;   // fused tick: [B][ho_stride_granules(N)] hand-off records (swarm_common.h)
 };
 
 constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
@@ -304,17 +303,23 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
             if (p == 1) reinterpret_cast<float4*>(rp_s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
             else if (p == 2) reinterpret_cast<float4*>(rp_sn)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
             else { rp_r[ri] = rew; rp_a[ri] = (uint8_t)action[ct]; }
-            if (HO && ho_pub) {   // write-through copy for this tick's TD wave (hand-off record)
-              float* rec = A.ho_rec + (size_t)d.gid * ho_stride_floats(N);
+            if (HO && ho_pub) {   // tagged write-through copy for this tick's TD waves (hand-off record)
+              unsigned long long* rec = A.ho_rec + (size_t)d.gid * ho_stride_granules(N);
+              const uint32_t tag = cc.tick + 1u;
               if (p == 1) {
-                st_sc1(rec + 4 * n, px[ct]); st_sc1(rec + 4 * n + 1, py[ct]);
-                st_sc1(rec + 4 * n + 2, vx[ct]); st_sc1(rec + 4 * n + 3, vy[ct]);
+                st_granule(rec + 4 * n, tag, __float_as_uint(px[ct]));
+                st_granule(rec + 4 * n + 1, tag, __float_as_uint(py[ct]));
+                st_granule(rec + 4 * n + 2, tag, __float_as_uint(vx[ct]));
+                st_granule(rec + 4 * n + 3, tag, __float_as_uint(vy[ct]));
               } else if (p == 2) {
-                float* r2 = rec + 4 * N + 4 * n;
-                st_sc1(r2, o[ct].px); st_sc1(r2 + 1, o[ct].py); st_sc1(r2 + 2, o[ct].vx); st_sc1(r2 + 3, o[ct].vy);
+                unsigned long long* r2 = rec + 4 * N + 4 * n;
+                st_granule(r2, tag, __float_as_uint(o[ct].px));
+                st_granule(r2 + 1, tag, __float_as_uint(o[ct].py));
+                st_granule(r2 + 2, tag, __float_as_uint(o[ct].vx));
+                st_granule(r2 + 3, tag, __float_as_uint(o[ct].vy));
               } else {
-                st_sc1(rec + 8 * N + n, rew);
-                st_sc1(rec + 9 * N + n, __int_as_float(action[ct]));
+                st_granule(rec + 8 * N + n, tag, __float_as_uint(rew));
+                st_granule(rec + 9 * N + n, tag, (uint32_t)action[ct]);
               }
             }
           }
@@ -337,12 +342,6 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       px[ct] = o[ct].px; py[ct] = o[ct].py; vx[ct] = o[ct].vx; vy[ct] = o[ct].vy;
     }
     hits_sum = hits_sum + hsum;
-    if (MODE == MODE_TICK && HO && ho_pub) {   // every lane's record stores done, then the flag
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (d.lane == 0)
-        __hip_atomic_store(A.ho_flags + d.gid, cc.tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      SWARM_RTSTAMP(25);
-    }
     if (it == 0) SWARM_STAMP(14);
     if (MODE == MODE_ROLLOUT && it == n_ticks - 1 && c == 0 && p == 0 && d.live) {
       if (A.out.avg_dist) A.out.avg_dist[d.gid] = avg;

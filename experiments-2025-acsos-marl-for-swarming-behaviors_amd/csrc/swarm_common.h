@@ -160,18 +160,20 @@ __host__ __device__ inline uint32_t sample_position(uint32_t g, const SampleKey&
 // ---------------------------------------------------------------- fused-tick hand-off
 // The fused training tick (swarm_tick.hip) runs the acting blocks beside the TD blocks.
 // A TD graph drawn from THIS tick's replay slot is the transition an acting wave is still
-// producing: that wave publishes it into an env-exclusive record (whole 128-B lines, so
-// no other producer shares a line) with write-through sc1 stores, waits for them
-// (vmcnt(0)), then sc1-stores the env's flag = tick + 1; the TD wave polls the flag with
-// sc1 loads and reads the record with sc1 loads only (MI355X_MICROARCH.md, inter-workgroup
-// visibility, "Valid forms", first table row).  Record: s [N][4], s' [N][4], r [N], a [N].
-__host__ __device__ constexpr int ho_stride_floats(int N) { return ((10 * N + 31) / 32) * 32; }
-__device__ inline void st_sc1(float* p, float v) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// producing: that wave publishes it as tagged granules — 8 bytes {tag = tick + 1, value},
+// each ONE aligned write-through (sc1) store — into an env-exclusive record (whole 128-B
+// lines); the TD wave re-reads its granules with sc1 loads until every tag matches, so
+// the data is its own flag: no producer drain, no flag, no second round trip
+// (cdna_hip_programming.md §6 Guideline 16, R2).  Tags never repeat (the tick counter
+// advances every tick), so no per-launch reset is needed.
+// Record of env e (granule index): s [N][4] at 4n + k, s' [N][4] at 4N + 4n + k, r at 8N + n,
+// a at 9N + n.
+__host__ __device__ constexpr int ho_stride_granules(int N) { return ((10 * N + 15) / 16) * 16; }
+__device__ inline void st_granule(unsigned long long* g, uint32_t tag, uint32_t value) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ inline float ld_sc1(const float* p) {
-  return __uint_as_float(
-      __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+__device__ inline unsigned long long ld_granule(const unsigned long long* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- small math

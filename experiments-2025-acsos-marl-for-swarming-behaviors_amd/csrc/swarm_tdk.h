@@ -100,9 +100,8 @@ struct TdSmem {
 struct TdFused {
   swarm_learner lr;
   swarm_adam_cfg hp;
-  const uint32_t* ho_flags;   // [B] publish stamps
-  const float* ho_rec;        // [B][ho_stride_floats(N)]
-  uint32_t* ho_err;           // bounded-wait overruns (0 in a correct run)
+  const unsigned long long* ho_rec;   // [B][ho_stride_granules(N)] tagged hand-off records
+  uint32_t* ho_err;                   // bounded-wait overruns (0 in a correct run)
 };
 constexpr int kHoSpinLimit = 1 << 18;   // polls (with s_sleep) before a hand-off wait gives up
 
@@ -216,39 +215,36 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     if (pending && (cc.tick % (uint32_t)X.hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
     else ptg.store(Ptg, threadIdx.x);
     // waves whose graphs wait for a hand-off are the tick's critical path: top issue priority
-    if (waited) {
-      const uint32_t stamp = cc.tick + 1u;
+    if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off)
+      const uint32_t tag = cc.tick + 1u;
       for (int spin = 0;; ++spin) {
-        if (wait) {
-          bool miss = false;
+        bool ok = true;
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct)
-            if (ho[ct])
-              miss = miss || __hip_atomic_load(X.ho_flags + gid[ct] % (uint32_t)B, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) != stamp;
-          wait = miss;
+        for (int ct = 0; ct < CT; ++ct) {
+          if (ho[ct]) {
+            const unsigned long long* rec = X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
+            const int j = min(jl[ct], N - 1);
+            const unsigned long long* sp = rec + (online ? 0 : 4 * N) + 4 * j;
+            const unsigned long long g0 = ld_granule(sp), g1 = ld_granule(sp + 1), g2 = ld_granule(sp + 2),
+                                     g3 = ld_granule(sp + 3);
+            const unsigned long long g4 = ld_granule(rec + (online ? 9 * N : 8 * N) + j);
+            ok = ok && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag && (uint32_t)(g2 >> 32) == tag &&
+                 (uint32_t)(g3 >> 32) == tag && (uint32_t)(g4 >> 32) == tag;
+            st[ct] = make_float4(__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1),
+                                 __uint_as_float((uint32_t)g2), __uint_as_float((uint32_t)g3));
+            if (online) act[ct] = nv[ct] ? (int)(uint32_t)g4 : 0;
+            else rew[ct] = __uint_as_float((uint32_t)g4);
+          }
         }
-        if (!__builtin_amdgcn_ballot_w64(wait)) break;
-        if (spin >= kHoSpinLimit) {   // never in a correct run: count it, read what is there
+        if (!__builtin_amdgcn_ballot_w64(!ok)) break;
+        if (spin >= kHoSpinLimit) {   // never in a correct run: count it, go on with what is there
           if (lane == 0) atomicAdd(X.ho_err, 1u);
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
-      asm volatile("" ::: "memory");   // the record loads stay behind the matched poll
       SWARM_RTSTAMP(10);
       __builtin_amdgcn_s_setprio(3);
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        if (ho[ct]) {
-          const float* rec = X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_floats(N);
-          const int j = min(jl[ct], N - 1);
-          const float* sp = rec + (online ? 0 : 4 * N) + 4 * j;
-          st[ct].x = ld_sc1(sp); st[ct].y = ld_sc1(sp + 1); st[ct].z = ld_sc1(sp + 2); st[ct].w = ld_sc1(sp + 3);
-          rew[ct] = ld_sc1(rec + 8 * N + j);
-          act[ct] = nv[ct] ? __float_as_int(ld_sc1(rec + 9 * N + j)) : 0;
-        }
-      }
     }
   }
   DFwd<NS> F;

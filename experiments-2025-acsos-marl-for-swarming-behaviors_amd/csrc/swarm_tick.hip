@@ -10,7 +10,7 @@
 // of the previous tick in registers, so neither waits on a launch boundary for the weights.
 // The only in-launch dependency is the reference's push-then-sample order: a TD graph drawn
 // from THIS tick's replay slot waits for the acting wave of its env, which publishes the
-// transition through the sc1 hand-off record (swarm_common.h).  Acting blocks never wait
+// transition as tagged write-through granules (swarm_common.h).  Acting blocks never wait
 // and have the lower block indices; the wait is bounded (kHoSpinLimit) and counted in the
 // workspace's error word, so the grid always drains.  Every other TD graph (slots written by
 // earlier ticks) runs concurrently with acting.
@@ -45,10 +45,9 @@ __global__ __launch_bounds__(256) void tick_kernel(const swarm_ctrl* __restrict_
 using namespace swarm;
 
 namespace {
-// workspace: [flags: B u32][err: 1 u32] (each rounded to 128 B), then the records
-size_t flags_bytes(int B) { return (((size_t)B * 4 + 127) / 128) * 128; }
+// workspace: [err: 1 u32, rounded to 128 B], then the tagged hand-off records
 size_t err_bytes() { return 128; }
-size_t rec_bytes(int B, int N) { return (size_t)B * ho_stride_floats(N) * 4; }
+size_t rec_bytes(int B, int N) { return (size_t)B * ho_stride_granules(N) * 8; }
 }  // namespace
 
 extern "C" {
@@ -61,7 +60,7 @@ int swarm_train_tick_supported(const swarm_config* cfg) {
 
 int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg) {
   if (!swarm_train_tick_supported(cfg)) return SWARM_E_UNSUPPORTED;
-  return (int64_t)(flags_bytes(cfg->n_envs) + err_bytes() + rec_bytes(cfg->n_envs, cfg->n_agents));
+  return (int64_t)(err_bytes() + rec_bytes(cfg->n_envs, cfg->n_agents));
 }
 
 int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
@@ -73,9 +72,8 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
     return SWARM_E_BADARG;
   const int B = cfg->n_envs, N = cfg->n_agents;
   char* ws = static_cast<char*>(workspace);
-  uint32_t* flags = reinterpret_cast<uint32_t*>(ws);
-  uint32_t* err = reinterpret_cast<uint32_t*>(ws + flags_bytes(B));
-  float* rec = reinterpret_cast<float*>(ws + flags_bytes(B) + err_bytes());
+  uint32_t* err = reinterpret_cast<uint32_t*>(ws);
+  unsigned long long* rec = reinterpret_cast<unsigned long long*>(ws + err_bytes());
 
   ActArgs a = {};
   a.B = B; a.N = N; a.scenario = cfg->scenario; a.graph = cfg->graph; a.k = cfg->knn_k; a.conv = cfg->conv;
@@ -85,7 +83,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
   a.replay = *replay;
   if (out) a.out = *out;
-  a.ho_flags = flags; a.ho_rec = rec;
+  a.ho_rec = rec;
 
   TdArgs t = {};
   t.S = hp->batch; t.B = B; t.N = N; t.graph = cfg->graph; t.k = cfg->knn_k; t.conv = cfg->conv;
@@ -96,7 +94,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   t.grad_scale = (float)(2.0 / ((double)hp->batch * (double)N));
 
   TdFused x = {};
-  x.lr = *lr; x.hp = *hp; x.ho_flags = flags; x.ho_rec = rec; x.ho_err = err;
+  x.lr = *lr; x.hp = *hp; x.ho_rec = rec; x.ho_err = err;
 
   const int n_act = (B + kActWPB - 1) / kActWPB;
   const int gs = N <= 8 ? 8 : 16;

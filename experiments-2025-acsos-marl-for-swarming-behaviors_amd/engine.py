@@ -154,7 +154,7 @@ class SwarmEngine:
             nb = self.lib.swarm_train_tick_workspace_bytes(ctypes_ref(self.cfg))
             check(int(min(nb, 0)), "swarm_train_tick_workspace_bytes")
             self.tick_ws = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
-            self._ho_err_off = -(-4 * n_envs // 128) * 128
+            self._ho_err_off = 0
         # per-tick outputs
         self.q = torch.zeros(n_envs, n_agents, 9, **f32)
         self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
