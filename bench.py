@@ -63,6 +63,22 @@ def complete_in_degree(N: int) -> float:
     return ((N - 1) * N + 1) / N
 
 
+def mean_in_degree(args, eng) -> float:
+    """Average in-degree of the bench graph: analytic for complete / kNN, measured on the
+    reset state for the radius graph (its degree depends on the formation)."""
+    N = args.agents
+    if args.graph == "complete":
+        return complete_in_degree(N)
+    if args.graph == "knn":
+        return (2 * N * args.knn_k + 1) / N
+    import swarm_amd
+    eng.reset(0)
+    obs = torch.cat([eng.state, torch.tensor([-0.8, 0.8], device=eng.state.device).expand(*eng.state.shape[:2], 2)], -1)
+    d = swarm_amd.create_radius_graph_from_observations(obs, N, args.radius)
+    from swarm_amd.graph import build_mult
+    return float(build_mult(d).float().sum().item()) / (args.envs * N)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,8 +88,9 @@ def parse():
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--scenario", default="GoTo")
     ap.add_argument("--conv", default="gat", choices=("gat", "gcn"))
-    ap.add_argument("--graph", default="complete", choices=("complete", "knn"))
+    ap.add_argument("--graph", default="complete", choices=("complete", "knn", "radius"))
     ap.add_argument("--knn-k", type=int, default=10)
+    ap.add_argument("--radius", type=float, default=0.3, help="neighbour radius of --graph radius")
     ap.add_argument("--mode", default="train", choices=("train", "act"),
                     help="train: fused training tick (headline); act: acting-only rollout with frozen "
                          "weights, eps 0 (Simulator-shaped, replicas only)")
@@ -119,7 +136,8 @@ def main():
     w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
     eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=shard.env_offset,
                                 world_size=world, process_group=pg, update_target_every=200,
-                                replay_capacity=1_000_000, conv=args.conv, graph=args.graph, knn_k=args.knn_k)
+                                replay_capacity=1_000_000, conv=args.conv, graph=args.graph, knn_k=args.knn_k,
+                                radius=args.radius)
     max_steps = 100
     if args.mode == "act":
         return bench_act(args, eng, world, rank, distributed, max_steps)
@@ -243,7 +261,7 @@ def main():
                              ("grad_reduce_kernel", eng.launch_grad_reduce)):
                 kt[name] = chain_us(fn)
 
-    d = complete_in_degree(N) if args.graph == "complete" else (2 * N * args.knn_k + 1) / N
+    d = mean_in_degree(args, eng)
     if args.conv == "gat":
         td_flops_launch = S * N * (2 * gat_fwd_flops(N, d) + td_bwd_flops(N, d))
     else:
@@ -295,7 +313,7 @@ def main():
                 "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference GoTo seed_0 weights)",
                 "config": {"workload": f"{scen} train tick: {N} agents x {B} envs/GPU, {args.conv.upper()}, "
-                                       f"{args.graph if args.graph == 'complete' else f'kNN-{args.knn_k}'} graph, "
+                                       f"{ {'complete': 'complete', 'knn': f'kNN-{args.knn_k}', 'radius': f'radius-{args.radius}'}[args.graph]} graph, "
                                        f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
                            "global_envs": B * world, "td_batch_per_gpu": S, "graph": args.graph, "conv": args.conv,
                            "parallelism": f"env-sharded dp{world}" + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce" if distributed else ""),
@@ -341,7 +359,7 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    d = complete_in_degree(N) if args.graph == "complete" else (2 * N * args.knn_k + 1) / N
+    d = mean_in_degree(args, eng)
     f_node = (gat_fwd_flops(N, d) if args.conv == "gat" else gcn_fwd_flops(N, d)) + 300   # + physics
     roof = None
     if not args.no_kernel_timing:   # one 100-tick rollout launch, HIP events on its stream
@@ -362,7 +380,7 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
                 "frac": ach / PEAK_FP32_TFLOPS, "traffic": None, "kernel": "act_kernel rollout (swarm_rollout)",
                 "algorithmic_flops_per_launch": flops, "launch_us": round(t_l * 1e6, 2)}
     if rank == 0:
-        g = args.graph if args.graph == "complete" else f"kNN-{args.knn_k}"
+        g = {"complete": "complete", "knn": f"kNN-{args.knn_k}", "radius": f"radius-{args.radius}"}[args.graph]
         line = {"metric": "env-steps/sec (agents×envs), acting-only rollout", "value": round(B * N * world * args.steps / elapsed, 1),
                 "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SWARM_LIB_PATH") or os.path.join(HERE, "libswarm_hip.so")
 
 SWARM_GOTO, SWARM_OBSTACLE_AVOIDANCE = 0, 1
-GRAPH_COMPLETE, GRAPH_KNN, GRAPH_DENSE = 0, 1, 2
+GRAPH_COMPLETE, GRAPH_KNN, GRAPH_DENSE, GRAPH_RADIUS = 0, 1, 2, 3
 CONV_GAT, CONV_GCN = 0, 1
 F_SHARED_RESET, F_RANDOM_OA = 1, 2
 N_PARAMS = 1673
@@ -24,13 +24,13 @@ ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
           -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class SwarmConfig(ctypes.Structure):
     _fields_ = [("n_envs", c_int32), ("n_agents", c_int32), ("scenario", c_int32), ("graph", c_int32),
                 ("knn_k", c_int32), ("conv", c_int32), ("env_offset", c_int32), ("flags", c_int32),
-                ("seed", c_uint64)]
+                ("seed", c_uint64), ("radius", c_float), ("pad", c_int32)]
 
 
 class SwarmReplay(ctypes.Structure):

@@ -70,6 +70,10 @@ __global__ __launch_bounds__(64) void graph_kernel(ActArgs A, uint8_t* __restric
     const uint32_t m = g.valid ? knn_mask<NS>(g, N, A.k, sm, kq[g.s]) : 0u;
     if (g.q == 0) sm.knn[g.s] = m;
     wave_lds_sync();
+  } else if (A.graph == SWARM_GRAPH_RADIUS) {
+    const uint32_t m = g.valid ? radius_mask_node<NS>(g.s, N, A.radius, sm) : 0u;
+    if (g.q == 0) sm.knn[g.s] = m;
+    wave_lds_sync();
   }
   int mult[NS];
   in_edges<NS>(g, N, A.graph, sm, nullptr, mult);
@@ -102,8 +106,9 @@ namespace {
 int check_cfg(const swarm_config* c) {
   if (!c || c->n_envs < 0 || c->n_agents < 1 || c->n_agents > 32) return SWARM_E_BADARG;
   if (c->scenario != SWARM_GOTO && c->scenario != SWARM_OBSTACLE_AVOIDANCE) return SWARM_E_BADARG;
-  if (c->graph < 0 || c->graph > 2 || (c->conv != SWARM_CONV_GAT && c->conv != SWARM_CONV_GCN)) return SWARM_E_BADARG;
+  if (c->graph < 0 || c->graph > 3 || (c->conv != SWARM_CONV_GAT && c->conv != SWARM_CONV_GCN)) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_KNN && (c->knn_k < 1 || c->knn_k > c->n_agents)) return SWARM_E_KNN_K;
+  if (c->graph == SWARM_GRAPH_RADIUS && !(c->radius > 0.0f)) return SWARM_E_BADARG;
   return 0;
 }
 
@@ -112,6 +117,7 @@ ActArgs make_args(const swarm_config* c) {
   a.B = c->n_envs; a.N = c->n_agents; a.scenario = c->scenario; a.graph = c->graph;
   a.k = c->knn_k; a.conv = c->conv; a.env_offset = c->env_offset; a.flags = c->flags;
   a.k0 = (uint32_t)(c->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(c->seed >> 32);
+  a.radius = c->radius;
   return a;
 }
 

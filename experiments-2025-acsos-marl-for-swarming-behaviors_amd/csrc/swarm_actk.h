@@ -18,6 +18,7 @@ enum { MODE_Q = 0, MODE_TICK = 1, MODE_ROLLOUT = 2, MODE_STEP = 3 };
 struct ActArgs {
   int B, N, scenario, graph, k, conv, env_offset, flags;
   uint32_t k0, k1;
+  float radius;            // SWARM_GRAPH_RADIUS
   const float* params;
   const float* x;          // MODE_Q node features [B*N][7]
   const uint8_t* dense;    // SWARM_GRAPH_DENSE multiplicity
@@ -185,7 +186,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       }
     }
     if (MODE != MODE_STEP) {
-      dl_forward<NS, 8>(P, d, N, graph, A.k, conv, A.dense, V, false, F);
+      dl_forward<NS, 8>(P, d, N, graph, A.k, A.radius, conv, A.dense, V, false, F);
     } else {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)

@@ -87,6 +87,8 @@ __device__ inline int in_mult(int u, int n, int N, int graph, const WSmall<NS>& 
   if (graph == SWARM_GRAPH_COMPLETE) return (ju != jn ? 1 : 0) + ((ju == 0 && jn == 0) ? 1 : 0);
   if (graph == SWARM_GRAPH_KNN)
     return (int)((sm.knn[u] >> jn) & 1u) + (int)((sm.knn[n] >> ju) & 1u) + ((ju == 0 && jn == 0) ? 1 : 0);
+  if (graph == SWARM_GRAPH_RADIUS)   // symmetric neighbour sets: one edge per ordered pair
+    return (int)((sm.knn[n] >> ju) & 1u) + ((ju == 0 && jn == 0) ? 1 : 0);
   return (int)dense[((size_t)gid * N + ju) * N + jn];
 }
 
@@ -106,10 +108,31 @@ __device__ inline void in_mults(int n, int N, int graph, const WSmall<NS>& sm, c
 #pragma unroll
     for (int j = 0; j < GS; ++j)
       m[j] = (tv && j < N) ? (int)((sm.knn[base + j] >> jn) & 1u) + (int)((kn >> j) & 1u) + (int)(j == 0 && jn == 0) : 0;
+  } else if (graph == SWARM_GRAPH_RADIUS) {
+    const uint32_t kn = sm.knn[min(n, NS - 1)];
+#pragma unroll
+    for (int j = 0; j < GS; ++j) m[j] = (tv && j < N) ? (int)((kn >> j) & 1u) + (int)(j == 0 && jn == 0) : 0;
   } else {
 #pragma unroll
     for (int j = 0; j < GS; ++j) m[j] = (tv && j < N) ? (int)dense[((size_t)gid * N + j) * N + jn] : 0;
   }
+}
+
+// radius-neighbour row of slot n over its graph: bit j = local node j != n with
+// |p_j - p_n| <= r (the kNN build's fp32 distance expression, simulator.py:18)
+template <int NS, int GS = NS>
+__device__ inline uint32_t radius_mask_node(int n, int N, float r, const WSmall<NS>& sm) {
+  const int base = (GS < NS) ? (n / GS) * GS : 0;
+  const int jn = (GS < NS) ? n % GS : n;
+  if (jn >= N) return 0u;
+  const float xi = sm.px[n], yi = sm.py[n];
+  uint32_t m = 0u;
+#pragma unroll
+  for (int j = 0; j < GS; ++j) {
+    const float d = norm2(sm.px[base + j] - xi, sm.py[base + j] - yi);
+    m |= (j < N && j != jn && d <= r) ? (1u << j) : 0u;
+  }
+  return m;
 }
 
 // kNN row of slot n over its graph (positions in sm; bit j = local node j).  q: GS
@@ -170,7 +193,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
 // padded LDS weight image.  Writes the H rows (and T / R rows if keep_tr) of V, the
 // per-node scalars of V.sm, and leaves F.t / F.zr / F.cf / F.q for the backward.
 template <int NS, int SB = -1, int GS = NS>
-__device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& d, int N, int graph, int k, int conv,
+__device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& d, int N, int graph, int k, float radius, int conv,
                                   const uint8_t* __restrict__ dense, const WView<NS>& V, bool keep_tr, DFwd<NS>& F) {
 #define DF_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
   constexpr int CT = DGeom<NS>::CT;
@@ -240,6 +263,13 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
         KV* q = reinterpret_cast<KV*>(&V.T[0][0]) + (n < NS ? n : 0) * GS;
         if (n < NS && p == 0) sm.knn[n] = (((GS < NS) ? n % GS : n) < N) ? knn_mask_node<NS, GS>(n, N, k, sm, q) : 0u;
       }
+    }
+    wave_lds_sync();
+  } else if (graph == SWARM_GRAPH_RADIUS) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int n = 16 * ct + c;
+      if (n < NS && p == 0) sm.knn[n] = radius_mask_node<NS, GS>(n, N, radius, sm);
     }
     wave_lds_sync();
   }

@@ -250,7 +250,9 @@ namespace {
 int check_td(const swarm_config* c, const swarm_adam_cfg* hp) {
   if (!c || !hp || c->n_agents < 1 || c->n_agents > 32 || c->n_envs < 1 || hp->batch < 1) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_DENSE) return SWARM_E_BADARG;
+  if (c->graph < 0 || c->graph > 3) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_KNN && (c->knn_k < 1 || c->knn_k > c->n_agents)) return SWARM_E_KNN_K;
+  if (c->graph == SWARM_GRAPH_RADIUS && !(c->radius > 0.0f)) return SWARM_E_BADARG;
   if (hp->world_size < 1 || hp->update_target_every < 1) return SWARM_E_BADARG;
   return 0;
 }
@@ -272,6 +274,7 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.S = hp->batch; a.B = cfg->n_envs; a.N = cfg->n_agents; a.graph = cfg->graph; a.k = cfg->knn_k;
   a.conv = cfg->conv; a.env_offset = cfg->env_offset;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(cfg->seed >> 32);
+  a.radius = cfg->radius;
   a.params = params; a.target = target; a.replay = *replay; a.ctrl = ctrl;
   a.sample_in = sample_in; a.sample_out = sample_out; a.slabs = slabs;
   a.gamma = hp->gamma;

@@ -50,6 +50,7 @@ struct TdLds {
 struct TdArgs {
   int S, B, N, graph, k, conv, env_offset;
   uint32_t k0, k1;
+  float radius;
   const float* params;
   const float* target;
   swarm_replay replay;
@@ -267,7 +268,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121).
   //      Everything after B1 waits for the target waves' y, so they issue first.
   if (!online && !waited) __builtin_amdgcn_s_setprio(2);
-  dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, conv, nullptr, V, online, F);
+  dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, A.radius, conv, nullptr, V, online, F);
   if (!online && p == 0) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {

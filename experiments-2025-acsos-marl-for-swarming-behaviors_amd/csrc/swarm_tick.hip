@@ -54,7 +54,10 @@ extern "C" {
 
 int swarm_train_tick_supported(const swarm_config* cfg) {
   if (!cfg || cfg->n_agents < 1 || cfg->n_agents > 16 || cfg->n_envs < 1) return 0;
-  return cfg->graph == SWARM_GRAPH_COMPLETE && (cfg->conv == SWARM_CONV_GAT || cfg->conv == SWARM_CONV_GCN) &&
+  if (cfg->graph == SWARM_GRAPH_KNN && (cfg->knn_k < 1 || cfg->knn_k > cfg->n_agents)) return 0;
+  if (cfg->graph == SWARM_GRAPH_RADIUS && !(cfg->radius > 0.0f)) return 0;
+  return (cfg->graph == SWARM_GRAPH_COMPLETE || cfg->graph == SWARM_GRAPH_KNN || cfg->graph == SWARM_GRAPH_RADIUS) &&
+         (cfg->conv == SWARM_CONV_GAT || cfg->conv == SWARM_CONV_GCN) &&
          (cfg->scenario == SWARM_GOTO || cfg->scenario == SWARM_OBSTACLE_AVOIDANCE);
 }
 
@@ -78,7 +81,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   ActArgs a = {};
   a.B = B; a.N = N; a.scenario = cfg->scenario; a.graph = cfg->graph; a.k = cfg->knn_k; a.conv = cfg->conv;
   a.env_offset = cfg->env_offset; a.flags = cfg->flags;
-  a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(cfg->seed >> 32);
+  a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(cfg->seed >> 32); a.radius = cfg->radius;
   a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = nullptr;
   a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
   a.replay = *replay;
@@ -87,7 +90,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
 
   TdArgs t = {};
   t.S = hp->batch; t.B = B; t.N = N; t.graph = cfg->graph; t.k = cfg->knn_k; t.conv = cfg->conv;
-  t.env_offset = cfg->env_offset; t.k0 = a.k0; t.k1 = a.k1;
+  t.env_offset = cfg->env_offset; t.k0 = a.k0; t.k1 = a.k1; t.radius = cfg->radius;
   t.params = lr->w_nxt; t.target = lr->target; t.replay = *replay; t.ctrl = ctrl;
   t.sample_in = nullptr; t.sample_out = sample_out; t.slabs = slabs;
   t.gamma = hp->gamma;
@@ -103,13 +106,16 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   hipStream_t st = (hipStream_t)stream;
   const float *g = lr->grad, *w = lr->w_cur, *m = lr->m_cur, *v = lr->v_cur;
   const bool oa = cfg->scenario == SWARM_OBSTACLE_AVOIDANCE;
-  const bool gat = cfg->conv == SWARM_CONV_GAT;
+  // complete graph (the reference's training graph): graph and conv fixed at compile time;
+  // kNN / radius training graphs: the runtime-switched kernel
+  const int spec = spec_of(cfg->graph, cfg->conv);
 #define SWARM_TICK_LAUNCH(NSA, GS, SC, SP) \
   hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP>), grid, block, 0, st, ctrl, state, g, w, m, v, B, N, n_act, a, t, x)
-#define SWARM_TICK_LAUNCH2(NSA, GS, SC)                                      \
-  do {                                                                        \
-    if (gat) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GAT);               \
-    else SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GCN);                   \
+#define SWARM_TICK_LAUNCH2(NSA, GS, SC)                                               \
+  do {                                                                                 \
+    if (spec == SPEC_COMPLETE_GAT) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GAT);  \
+    else if (spec == SPEC_COMPLETE_GCN) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GCN); \
+    else SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_RUNTIME);                                 \
   } while (0)
   if (N <= 8) {
     if (oa) SWARM_TICK_LAUNCH2(8, 8, SWARM_OBSTACLE_AVOIDANCE);

@@ -173,6 +173,7 @@ __device__ inline uint32_t knn_mask(const WGeom<NS>& g, int N, int k, const WSma
 // multiplicity m(u -> s) of every source slot u (target = this lane's slot)
 //   complete (train_gcn_dqn.py:101-108): u != v pairs plus one (0, 0) edge
 //   kNN (simulator.py:15-24): (i -> j) and (j -> i) for j in S_i, plus (0, 0)
+//   radius: u -> s for u != s within the radius (symmetric), plus (0, 0)
 //   dense: caller-supplied [B][N][N] uint8
 template <int NS>
 __device__ inline void in_edges(const WGeom<NS>& g, int N, int graph, const WSmall<NS>& sm,
@@ -187,6 +188,8 @@ __device__ inline void in_edges(const WGeom<NS>& g, int N, int graph, const WSma
         m = (u != s ? 1 : 0) + ((u == 0 && s == 0) ? 1 : 0);
       } else if (graph == SWARM_GRAPH_KNN) {
         m = (int)((sm.knn[u] >> s) & 1u) + (int)((ks >> u) & 1u) + ((u == 0 && s == 0) ? 1 : 0);
+      } else if (graph == SWARM_GRAPH_RADIUS) {
+        m = (int)((sm.knn[s] >> u) & 1u) + ((u == 0 && s == 0) ? 1 : 0);
       } else {
         m = (int)dense[((size_t)g.gid * N + u) * N + s];
       }

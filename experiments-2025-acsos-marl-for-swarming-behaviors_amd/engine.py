@@ -40,7 +40,7 @@ from ._lib import (CTRL, N_PARAMS, SwarmActOut, SwarmAdamCfg, SwarmConfig, Swarm
 
 SCENARIOS = {"GoTo": _lib.SWARM_GOTO, "ObstacleAvoidance": _lib.SWARM_OBSTACLE_AVOIDANCE,
              "go_to": _lib.SWARM_GOTO, "obstacle_avoidance": _lib.SWARM_OBSTACLE_AVOIDANCE}
-GRAPHS = {"complete": _lib.GRAPH_COMPLETE, "knn": _lib.GRAPH_KNN}
+GRAPHS = {"complete": _lib.GRAPH_COMPLETE, "knn": _lib.GRAPH_KNN, "radius": _lib.GRAPH_RADIUS}
 CONVS = {"gat": _lib.CONV_GAT, "gcn": _lib.CONV_GCN}
 
 PARAM_ORDER = (
@@ -90,7 +90,7 @@ def glorot_init(generator: torch.Generator) -> torch.Tensor:
 
 class SwarmEngine:
     def __init__(self, scenario="GoTo", n_agents: int = 8, n_envs: int = 1024, *, seed: int = 0,
-                 graph: str = "complete", knn_k: int = 10, conv: str = "gat", params=None,
+                 graph: str = "complete", knn_k: int = 10, conv: str = "gat", params=None, radius: float = 0.3,
                  batch: Optional[int] = None, gamma: float = 0.99, lr: float = 1e-3, betas=(0.9, 0.999),
                  adam_eps: float = 1e-8, max_norm: float = 1.0, update_target_every: int = 200,
                  replay_capacity: int = 1_000_000, env_offset: int = 0, world_size: int = 1,
@@ -103,7 +103,7 @@ class SwarmEngine:
         sid = SCENARIOS[scenario] if isinstance(scenario, str) else int(scenario)
         flags = (_lib.F_SHARED_RESET if shared_reset else 0) | (_lib.F_RANDOM_OA if random_oa else 0)
         self.cfg = SwarmConfig(n_envs, n_agents, sid, GRAPHS[graph], knn_k, CONVS[conv], env_offset, flags,
-                               seed & 0xFFFFFFFFFFFFFFFF)
+                               seed & 0xFFFFFFFFFFFFFFFF, float(radius), 0)
         self.B, self.N = n_envs, n_agents
         self.scenario_id = sid
         self.batch = n_envs if batch is None else batch

@@ -67,7 +67,8 @@ class GCN(nn.Module):
         q = torch.empty(M, 9, dtype=torch.float32, device=x.device)
         if data.swarm is not None:
             m = data.swarm
-            cfg = _lib.SwarmConfig(m["n_graphs"], m["n_nodes"], 0, m["graph"], m["k"], conv, 0, 0, 0)
+            cfg = _lib.SwarmConfig(m["n_graphs"], m["n_nodes"], 0, m["graph"], m["k"], conv, 0, 0, 0,
+                                   float(m.get("radius", 0.0)), 0)
             check(lib.swarm_q_forward(_lib_byref(cfg), ptr(params), ptr(x), None, ptr(q), stream_ptr()),
                   "swarm_q_forward")
         else:

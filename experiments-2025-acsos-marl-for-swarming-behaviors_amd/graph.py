@@ -12,6 +12,10 @@ Builders:
 * ``create_knn_graph_from_observations(obs, n_agents, k)`` — evaluation graph,
   simulator.py:9-26: per node its k nearest (torch.topk set semantics, itself
   included), edges both ways, plus (0, 0).
+* ``create_radius_graph_from_observations(obs, n_agents, radius)`` — the north_star's
+  radius-neighbour graph (not in the reference; SURVEY §8(f) row 3, parity unpinned):
+  edge (i, j) for every j != i with |p_i - p_j| <= radius (the kNN build's fp32 distance),
+  plus (0, 0) as both reference builders append it.
 """
 from __future__ import annotations
 
@@ -62,7 +66,8 @@ class Batch(Data):
         xs = [d.x for d in data_list]
         x = torch.cat(xs, dim=0)
         metas = [d.swarm for d in data_list]
-        if all(m is not None for m in metas) and len({(m["n_nodes"], m["graph"], m["k"]) for m in metas}) == 1:
+        if all(m is not None for m in metas) and len({(m["n_nodes"], m["graph"], m["k"], m.get("radius", 0.0))
+                                                      for m in metas}) == 1:
             m = dict(metas[0])
             m["n_graphs"] = sum(mm["n_graphs"] for mm in metas)
             b = Batch(x, None, swarm=m)
@@ -101,9 +106,18 @@ def create_knn_graph_from_observations(observations, num_agents: int, k: int = 1
     return Data(x, None, swarm=dict(n_graphs=x.shape[0] // num_agents, n_nodes=num_agents, graph=_lib.GRAPH_KNN, k=k))
 
 
+def create_radius_graph_from_observations(observations, num_agents: int, radius: float) -> Data:
+    if not radius > 0.0:
+        raise ValueError("radius must be > 0")
+    x = _node_features(observations)
+    return Data(x, None, swarm=dict(n_graphs=x.shape[0] // num_agents, n_nodes=num_agents, graph=_lib.GRAPH_RADIUS,
+                                    k=0, radius=float(radius)))
+
+
 def graph_config(data: Data, scenario: int = 0, conv: int = _lib.CONV_GAT) -> _lib.SwarmConfig:
     m = data.swarm
-    return _lib.SwarmConfig(m["n_graphs"], m["n_nodes"], scenario, m["graph"], m["k"], conv, 0, 0, 0)
+    return _lib.SwarmConfig(m["n_graphs"], m["n_nodes"], scenario, m["graph"], m["k"], conv, 0, 0, 0,
+                            float(m.get("radius", 0.0)), 0)
 
 
 def build_mult(data: Data) -> torch.Tensor:

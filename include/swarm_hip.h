@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 3
+#define SWARM_ABI_VERSION 4
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
@@ -30,7 +30,7 @@ extern "C" {
 #define SWARM_E_UNSUPPORTED (-4) /* configuration has no fused-tick kernel (use the 3-launch tick) */
 
 enum swarm_scenario { SWARM_GOTO = 0, SWARM_OBSTACLE_AVOIDANCE = 1 };
-enum swarm_graph { SWARM_GRAPH_COMPLETE = 0, SWARM_GRAPH_KNN = 1, SWARM_GRAPH_DENSE = 2 };
+enum swarm_graph { SWARM_GRAPH_COMPLETE = 0, SWARM_GRAPH_KNN = 1, SWARM_GRAPH_DENSE = 2, SWARM_GRAPH_RADIUS = 3 };
 enum swarm_conv { SWARM_CONV_GAT = 0, SWARM_CONV_GCN = 1 };
 
 /* Static description of a batch of vectorised environments (one rank's shard). */
@@ -39,12 +39,16 @@ typedef struct swarm_config {
   int32_t n_agents;     /* N: agents per environment, 1..32                             */
   int32_t scenario;     /* swarm_scenario                                               */
   int32_t graph;        /* swarm_graph: complete (train_gcn_dqn.py:101-108), kNN (simulator.py:15-24),
-                           or DENSE = caller-supplied multiplicity matrix [B][N][N] uint8  */
+                           DENSE = caller-supplied multiplicity matrix [B][N][N] uint8, or
+                           RADIUS = radius-neighbour graph (north_star):
+                           edge u -> v for u != v with |p_u - p_v| <= radius, plus (0, 0)  */
   int32_t knn_k;        /* k of the kNN graph (reference code: 10, recorded data: 5)    */
   int32_t conv;         /* swarm_conv: GAT (the reference's GCN class) or GCNConv (a13) */
   int32_t env_offset;   /* global index of env 0 (rank sharding; keys the RNG)          */
   int32_t flags;        /* SWARM_F_* bits                                               */
   uint64_t seed;        /* Philox key                                                   */
+  float radius;         /* neighbour radius of SWARM_GRAPH_RADIUS (> 0)                 */
+  int32_t pad;
 } swarm_config;
 
 #define SWARM_F_SHARED_RESET 1   /* one reset centre for all envs (go_to_position_scenario.py:88) */
@@ -185,7 +189,7 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
  * :170-172) read the acting waves' write-through hand-off records in `workspace`
  * (swarm_train_tick_workspace_bytes; zero it whenever ctrl is (re)initialised).  Follow with
  * swarm_reduce_advance [-> all-reduce(grad)].  Bit-identical to the 3-launch sequence.
- * Complete training graph, GAT or GCNConv, n_agents <= 16; else SWARM_E_UNSUPPORTED. */
+ * Complete, kNN or radius training graph, GAT or GCNConv, n_agents <= 16; else SWARM_E_UNSUPPORTED. */
 int swarm_train_tick_supported(const swarm_config* cfg);
 int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg);
 int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,

@@ -270,6 +270,36 @@ def knn_sets(pos: torch.Tensor, k: int) -> torch.Tensor:
     return out
 
 
+def radius_sets(pos: torch.Tensor, radius: float) -> torch.Tensor:
+    """[B,N,2] -> bool [B, N(i), N(j)]: j != i with |p_j - p_i| <= radius.  The radius-neighbour
+    graph of the north_star (not in the reference, SURVEY §8(f) row 3: parity unpinned); the
+    distance is the kNN build's own expression (simulator.py:18) so the sets are bit-exact."""
+    B, N, _ = pos.shape
+    out = torch.zeros(B, N, N, dtype=torch.bool)
+    r = torch.tensor(radius, dtype=torch.float32)
+    for b in range(B):
+        for i in range(N):
+            d = torch.linalg.norm(pos[b, :, :2] - pos[b, i, :2], dim=1)
+            out[b, i] = d <= r
+            out[b, i, i] = False
+    return out
+
+
+def radius_edge_index(pos: torch.Tensor, radius: float) -> torch.Tensor:
+    """Edge-list form for one env (pos [N,2]): (i, j) for j in R(i), then (0, 0)."""
+    s = radius_sets(pos[None], radius)[0]
+    e = [[i, j] for i in range(pos.shape[0]) for j in range(pos.shape[0]) if bool(s[i, j])]
+    e.append([0, 0])
+    return torch.tensor(e, dtype=torch.long).t().contiguous()
+
+
+def multiplicity_radius(sets: torch.Tensor) -> torch.Tensor:
+    """m(u->v) = [v in R(u)] + [u=v=0]; R is symmetric, so every ordered pair appears once."""
+    m = sets.to(torch.float32).clone()
+    m[:, 0, 0] += 1.0
+    return m
+
+
 def multiplicity_complete(B: int, N: int) -> torch.Tensor:
     """m[b,u,v] = #edges u->v of the training graph."""
     m = torch.ones(B, N, N) - torch.eye(N).expand(B, N, N)
@@ -418,6 +448,7 @@ def egreedy(q: torch.Tensor, eps: float, seed: int, tick: int, env_offset: int =
 # ---------------------------------------------------------------------------
 GRAPH_COMPLETE = 0
 GRAPH_KNN = 1
+GRAPH_RADIUS = 3     # include/swarm_hip.h (2 = caller-supplied dense multiplicity)
 
 
 @dataclass
@@ -430,14 +461,20 @@ class TickOut:
     mult: torch.Tensor
 
 
+def graph_multiplicity(pos, graph: int, k: int = 0, radius: float = 0.0) -> torch.Tensor:
+    B, N, _ = pos.shape
+    if graph == GRAPH_COMPLETE:
+        return multiplicity_complete(B, N)
+    if graph == GRAPH_RADIUS:
+        return multiplicity_radius(radius_sets(pos, radius))
+    return multiplicity_knn(knn_sets(pos, k))
+
+
 def act_tick(params: dict, pos, vel, scenario: int, graph: int, k: int, eps: float,
-             seed: int, tick: int, conv: str = "gat", env_offset: int = 0) -> TickOut:
+             seed: int, tick: int, conv: str = "gat", env_offset: int = 0, radius: float = 0.0) -> TickOut:
     B, N, _ = pos.shape
     x = node_features(pos, vel)
-    if graph == GRAPH_COMPLETE:
-        mult = multiplicity_complete(B, N)
-    else:
-        mult = multiplicity_knn(knn_sets(pos, k))
+    mult = graph_multiplicity(pos, graph, k, radius)
     if conv == "gat":
         q = q_forward_dense(params, x, mult)
     else:

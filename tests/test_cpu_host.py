@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     for n in sorted(names):
         assert hasattr(raw, n), n
     assert names == set(L.EXPORTED)
-    assert lib.swarm_abi_version() == 3 and lib.swarm_n_params() == O.N_PARAMS
+    assert lib.swarm_abi_version() == 4 and lib.swarm_n_params() == O.N_PARAMS
 
 
 def test_topk_emulation_matches_torch_fixture():
@@ -105,7 +105,8 @@ def test_dense_forward_equals_edge_list_forward(golden_weights, n):
     pos = torch.randn(B, n, 2, generator=g) * 0.3
     vel = torch.randn(B, n, 2, generator=g) * 0.1
     x = O.node_features(pos, vel)
-    for mult in (O.multiplicity_complete(B, n), O.multiplicity_knn(O.knn_sets(pos, min(3, n)))):
+    for mult in (O.multiplicity_complete(B, n), O.multiplicity_knn(O.knn_sets(pos, min(3, n))),
+                 O.multiplicity_radius(O.radius_sets(pos, 0.3))):
         qd = O.q_forward_dense(params, x, mult)
         qe = O.q_forward_edges(params, x.reshape(B * n, 7), O.edge_index_from_multiplicity(mult))
         assert_close_rel(qd.reshape(B * n, 9), qe, 1e-5, 'dense vs edge-list Q')
@@ -124,6 +125,30 @@ def test_edge_builders_match_multiplicity():
     for s, d in ec.t().tolist():
         cnt[s, d] += 1
     assert torch.equal(cnt, O.multiplicity_complete(1, 6)[0])
+
+
+def test_radius_builders_match_multiplicity():
+    """Radius-neighbour graph (north_star; not in the reference): symmetric sets without
+    self-pairs, the edge list and the multiplicity agree, and (0, 0) is appended."""
+    pos = torch.tensor(O.grid_offsets(9), dtype=torch.float32)
+    for r in (0.1, 0.15, 0.22, 1.0):
+        sets = O.radius_sets(pos[None], r)[0]
+        assert torch.equal(sets, sets.t()) and not sets.diagonal().any()
+        ei = O.radius_edge_index(pos, r)
+        cnt = torch.zeros(9, 9)
+        for s_, d_ in ei.t().tolist():
+            cnt[s_, d_] += 1
+        assert torch.equal(cnt, O.multiplicity_radius(sets[None])[0])
+    assert int(O.radius_sets(pos[None], 1.0)[0].sum()) == 9 * 8
+
+
+def test_radius_graph_host_builder():
+    import swarm_amd
+    obs = {f"agent{i}": torch.randn(3, 6) for i in range(4)}
+    d = swarm_amd.create_radius_graph_from_observations(obs, 4, 0.5)
+    assert d.swarm["graph"] == 3 and d.swarm["radius"] == 0.5 and d.x.shape == (12, 7)
+    with pytest.raises(ValueError):
+        swarm_amd.create_radius_graph_from_observations(obs, 4, 0.0)
 
 
 def test_td_step_oracle_reduces_loss(golden_weights):

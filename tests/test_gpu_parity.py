@@ -106,6 +106,29 @@ def test_knn_graph_bit_exact(sw, N, k):
         assert torch.equal(mult[: B * N * N].view(B, N, N).cpu().float(), O.multiplicity_complete(B, N))
 
 
+@pytest.mark.parametrize("N,radius", [(5, 0.15), (8, 0.15), (8, 0.3), (12, 0.2), (16, 0.25), (29, 0.2)])
+def test_radius_graph_bit_exact(sw, N, radius):
+    """Radius-neighbour graph (north_star; not in the reference, parity unpinned): the
+    neighbour sets are bit-exact against the oracle, including the reset grid's pairs at
+    exactly the grid spacing (0.15) and jittered formations."""
+    import ctypes
+    from swarm_amd import _lib
+    B = 128
+    lib = _lib.load()
+    for tight in (True, False):
+        pos, vel = _rand_state(B, N, N * 7 + int(radius * 100), tight=tight)
+        x = O.node_features(pos, vel).reshape(B * N, 7)
+        mult = torch.zeros((B * N * N + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
+        cfg = _lib.SwarmConfig(B, N, 0, _lib.GRAPH_RADIUS, 0, 0, 0, 0, 0, radius, 0)
+        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
+        got = mult[: B * N * N].view(B, N, N).cpu().float()
+        ref = O.multiplicity_radius(O.radius_sets(pos, radius))
+        assert torch.equal(got, ref)
+        assert 0 < int((ref > 0).sum()) - B < B * N * (N - 1)   # neither empty nor complete
+    cfg.radius = 0.0
+    assert lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()) == -1
+
+
 def test_knn_k_larger_than_n_raises(sw):
     obs = {f"agent{i}": torch.randn(2, 6) for i in range(4)}
     with pytest.raises(RuntimeError):
@@ -115,7 +138,7 @@ def test_knn_k_larger_than_n_raises(sw):
 # ------------------------------------------------------------------ Q forward
 @pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
 @pytest.mark.parametrize("N", [1, 5, 8, 12, 20])
-@pytest.mark.parametrize("graph", ["complete", "knn"])
+@pytest.mark.parametrize("graph", ["complete", "knn", "radius"])
 def test_q_forward_parity(sw, golden_weights, scen, N, graph):
     B = 100
     model = sw.GCN(7, 32, 9)
@@ -126,9 +149,12 @@ def test_q_forward_parity(sw, golden_weights, scen, N, graph):
     if graph == "complete":
         data = sw.create_graph_from_observations(obs)
         mult = O.multiplicity_complete(B, N)
-    else:
+    elif graph == "knn":
         data = sw.create_knn_graph_from_observations(obs, N, k)
         mult = O.multiplicity_knn(O.knn_sets(pos, k))
+    else:
+        data = sw.create_radius_graph_from_observations(obs, N, 0.3)
+        mult = O.multiplicity_radius(O.radius_sets(pos, 0.3))
     q = model(data).cpu().view(B, N, 9)
     ref = O.q_forward_dense(O.unflatten_params(_params(golden_weights, scen, N % 10)), O.node_features(pos, vel), mult)
     assert_close_rel(q, ref, 1e-5, "Q")
@@ -201,19 +227,21 @@ def test_gpu_reproduces_recorded_reference_actions(sw, golden_weights, trajector
 @pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
 @pytest.mark.parametrize("N,graph,k,conv", [(8, "complete", 0, "gat"), (12, "knn", 10, "gat"), (5, "knn", 5, "gat"),
                                            (20, "complete", 0, "gat"), (29, "knn", 6, "gat"),
-                                           (8, "complete", 0, "gcn"), (12, "complete", 0, "gcn"), (7, "knn", 4, "gcn")])
+                                           (8, "complete", 0, "gcn"), (12, "complete", 0, "gcn"), (7, "knn", 4, "gcn"),
+                                           (8, "radius", 0, "gat"), (12, "radius", 0, "gcn"), (20, "radius", 0, "gat")])
 def test_act_tick_parity(sw, golden_weights, scen, N, graph, k, conv):
     B = 150
     p = _params(golden_weights, scen, 7)
+    radius = 0.25
     eng = sw.SwarmEngine(scen, N, B, seed=11, params=p, graph=graph, knn_k=max(k, 1), eps=0.35,
-                         replay_capacity=4 * B, conv=conv)
+                         replay_capacity=4 * B, conv=conv, radius=radius)
     pos, vel = _rand_state(B, N, 21, tight=(N == 5))
     eng.state.copy_(torch.cat([pos, vel], -1).cuda())
     eng.ctrl[0] = 5   # tick
     eng.act(push=True)
     torch.cuda.synchronize()
-    ref = O.act_tick(O.unflatten_params(p), pos, vel, SCEN[scen], O.GRAPH_COMPLETE if graph == "complete" else O.GRAPH_KNN,
-                     k, 0.35, 11, 5, conv=conv)
+    gid = {"complete": O.GRAPH_COMPLETE, "knn": O.GRAPH_KNN, "radius": O.GRAPH_RADIUS}[graph]
+    ref = O.act_tick(O.unflatten_params(p), pos, vel, SCEN[scen], gid, k, 0.35, 11, 5, conv=conv, radius=radius)
     assert_close_rel(eng.q.cpu(), ref.q, 1e-5, "Q")
     clear = _tie_mask(ref.q) | ref.explore[:, None]
     assert ref.explore.any() and (~ref.explore).any()
@@ -263,6 +291,7 @@ def _fill_replay(eng, seed):
     ("go_to", 5, 7, "complete", 0, "gat"), ("go_to", 8, 256, "complete", 0, "gat"),
     ("go_to", 20, 9, "complete", 0, "gat"), ("obstacle_avoidance", 29, 5, "complete", 0, "gat"),
     ("obstacle_avoidance", 12, 24, "knn", 5, "gat"), ("go_to", 20, 6, "knn", 10, "gat"),
+    ("go_to", 8, 32, "radius", 0, "gat"), ("obstacle_avoidance", 12, 24, "radius", 0, "gat"),
     # a13 GCNConv variant (C5's "GCN vs GAT"; parity unpinned: checked against the oracle's autograd only)
     ("go_to", 8, 64, "complete", 0, "gcn"), ("obstacle_avoidance", 12, 40, "complete", 0, "gcn"),
     ("obstacle_avoidance", 5, 33, "complete", 0, "gcn"), ("go_to", 20, 9, "complete", 0, "gcn")])
@@ -272,7 +301,7 @@ def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k, conv):
     p = _params(golden_weights, scen, 5)
     tgt = _params(golden_weights, scen, 6)
     eng = sw.SwarmEngine(scen, N, B, seed=2, params=p, batch=S, replay_capacity=cap * B, update_target_every=1000,
-                         graph=graph, knn_k=max(k, 1), conv=conv)
+                         graph=graph, knn_k=max(k, 1), conv=conv, radius=0.5)
     eng.target.copy_(tgt.cuda())
     _fill_replay(eng, S)
     idx = torch.randperm(cap * B, generator=torch.Generator().manual_seed(S))[:S].to(torch.int32)
@@ -287,6 +316,9 @@ def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k, conv):
     if graph == "knn":   # per-graph kNN edge lists (simulator.py:15-24), offset like Batch.from_data_list
         ei = torch.cat([O.knn_edge_index(s[g, :, :2], k) + g * N for g in range(S)], dim=1)
         ein = torch.cat([O.knn_edge_index(s1[g, :, :2], k) + g * N for g in range(S)], dim=1)
+    elif graph == "radius":
+        ei = torch.cat([O.radius_edge_index(s[g, :, :2], 0.5) + g * N for g in range(S)], dim=1)
+        ein = torch.cat([O.radius_edge_index(s1[g, :, :2], 0.5) + g * N for g in range(S)], dim=1)
     ref = O.td_step(p, tgt, torch.zeros_like(p), torch.zeros_like(p), 0, s, a, r, s1, edge_index=ei, edge_index_next=ein,
                     conv=conv)
     grad = eng.grad.cpu()
@@ -400,16 +432,20 @@ def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
     assert torch.equal(a.state, b.state) and torch.equal(a.rep_s, b.rep_s)
 
 
-@pytest.mark.parametrize("scen,N,conv,B,slots", [("GoTo", 8, "gat", 64, 4), ("GoTo", 5, "gat", 96, 1),
-                                                  ("ObstacleAvoidance", 12, "gat", 64, 3),
-                                                  ("ObstacleAvoidance", 16, "gcn", 40, 2),
-                                                  ("GoTo", 8, "gcn", 1024, 977)])
-def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, conv, B, slots):
+@pytest.mark.parametrize("scen,N,conv,B,slots,graph", [("GoTo", 8, "gat", 64, 4, "complete"),
+                                                        ("GoTo", 5, "gat", 96, 1, "complete"),
+                                                        ("ObstacleAvoidance", 12, "gat", 64, 3, "complete"),
+                                                        ("ObstacleAvoidance", 16, "gcn", 40, 2, "complete"),
+                                                        ("GoTo", 8, "gcn", 1024, 977, "complete"),
+                                                        ("GoTo", 8, "gat", 64, 2, "knn"),
+                                                        ("ObstacleAvoidance", 12, "gat", 48, 2, "radius")])
+def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, conv, B, slots, graph):
     """swarm_train_tick (acting and TD blocks in one launch, TD graphs of the tick's own slot
     read through the hand-off records) == the 3-launch tick, bit for bit, every tick.  Small
     rings make most draws come from the slot being written (slots = 1: all of them)."""
     p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 2)
-    kw = dict(seed=9, params=p, batch=B, eps=0.3, update_target_every=3, replay_capacity=slots * B, conv=conv)
+    kw = dict(seed=9, params=p, batch=B, eps=0.3, update_target_every=3, replay_capacity=slots * B, conv=conv,
+              graph=graph, knn_k=5, radius=0.25)
     a = sw.SwarmEngine(scen, N, B, **kw)
     b = sw.SwarmEngine(scen, N, B, **kw)
     assert a.fused

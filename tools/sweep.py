@@ -24,6 +24,9 @@ RUNS += [
     ("C2 GoTo 8x1024 GAT act complete", ["--mode", "act"]),
     ("C3 OA 12x1024 GAT act kNN-10", ["--mode", "act", "--scenario", "ObstacleAvoidance", "--agents", "12",
                                       "--graph", "knn", "--knn-k", "10"]),
+    # the north_star's radius-neighbour graph (not in the reference; 3-launch tick for training)
+    ("C2 GoTo 8x1024 GAT act radius-0.3", ["--mode", "act", "--graph", "radius", "--radius", "0.3"]),
+    ("C2 GoTo 8x1024 GAT train radius-0.3", ["--graph", "radius", "--radius", "0.3"]),
 ]
 
 if len(sys.argv) > 2:
