@@ -4,7 +4,9 @@ kNN graph -> GAT -> argmax -> env.step with frozen weights and records per-tick
 positions, average distance and hits; the CSV outputs keep the reference's
 layout (``result.csv``, ``positions/positions_episode_{e}_{x,y}.csv``,
 ``data/distances_episode_{e}.csv``).  ``knn_k`` defaults to the code's 10; the
-reference's committed outputs were produced with 5.
+reference's committed outputs were produced with 5.  ``graph="radius"`` with
+``radius=r`` evaluates on the north_star's radius-neighbour graph instead (not in the
+reference).
 With ``num_envs`` > 1, metrics are averaged over envs and trajectories of env 0
 are written.
 """
@@ -21,7 +23,8 @@ from . import _lib
 
 
 class Simulator:
-    def __init__(self, env, model, episodes, env_name, seed, output_dir="test_stats/", render=False, knn_k: int = 10):
+    def __init__(self, env, model, episodes, env_name, seed, output_dir="test_stats/", render=False, knn_k: int = 10,
+                 graph: str = "knn", radius: float = 0.3):
         self.env = env
         self.model = model
         self.episode_rewards = []
@@ -34,19 +37,23 @@ class Simulator:
         self.output_dir = output_dir
         self.render = render
         self.knn_k = knn_k
+        if graph not in ("knn", "radius"):
+            raise ValueError("graph must be 'knn' (simulator.py:15-24) or 'radius'")
+        self.graph = _lib.GRAPH_KNN if graph == "knn" else _lib.GRAPH_RADIUS
+        self.radius = float(radius)
         self.all_positions_x = []
         self.all_positions_y = []
         self.all_distances = []
         self.all_hits = []
 
     def run_simulation(self):
-        if self.knn_k > self.env.n_agents:
+        if self.graph == _lib.GRAPH_KNN and self.knn_k > self.env.n_agents:
             raise RuntimeError("selected index k out of range")
         eng = self.env.engine
         params = self.model.flat_params(eng.device)
         conv = _lib.CONV_GAT if getattr(self.model, "conv", "gat") == "gat" else _lib.CONV_GCN
-        saved = (eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv)
-        eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv = _lib.GRAPH_KNN, self.knn_k, conv
+        saved = (eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius)
+        eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius = self.graph, self.knn_k, conv, self.radius
         T = self.env.max_steps
         try:
             for episode in range(self.episodes):
@@ -68,7 +75,7 @@ class Simulator:
                 self.distance_at_the_beginning.append(dist[0])
                 self.episode_rewards.append(float(total_reward) / T)
         finally:
-            eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv = saved
+            eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius = saved
         self.save_metrics_to_csv()
 
     def save_metrics_to_csv(self):

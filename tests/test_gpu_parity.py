@@ -518,6 +518,10 @@ def test_simulator_and_trainer_smoke(sw, golden_weights, tmp_path):
     rows = list(csv.reader(open(tmp_path / "sim" / "result.csv")))
     assert rows[0] == ["Episode", "Reward", "Collisions", "Distance (end)", "Distance (beginning)"] and len(rows) == 3
     assert (tmp_path / "sim" / "positions" / "positions_episode_1_y.csv").exists()
+    sim_r = sw.Simulator(env, model, 1, "obstacle_avoidance", 1, output_dir=str(tmp_path / "sim_r"), graph="radius",
+                         radius=0.3)
+    sim_r.run_simulation()
+    assert len(list(csv.reader(open(tmp_path / "sim_r" / "result.csv")))) == 2
     env2 = sw.make_env(sw.GoToPositionScenario(), num_envs=4, continuous_actions=False, max_steps=10,
                        dict_spaces=True, seed=0, n_agents=5)
     tr = sw.DQNTrainer(env2, 0, str(tmp_path / "models"), str(tmp_path / "stats"), "GoTo", batch_size=8)
