@@ -220,6 +220,28 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       }
     }
 
+    // fused tick: this env's transition is in the tick's TD batch -> publish it as tagged
+    // write-through granules as soon as each part exists (swarm_common.h hand-off record):
+    // s and a now (the online TD wave starts its forward), s' after the integrator (the
+    // target TD wave's forward input), r after the reward (needed only for y)
+    unsigned long long* ho_r = nullptr;
+    const uint32_t ho_tag = cc.tick + 1u;
+    if (MODE == MODE_TICK && HO && ho_pub) {
+      ho_r = A.ho_rec + (size_t)d.gid * ho_stride_granules(N);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int n = 16 * ct + c;
+        if (valid[ct]) {
+          if (p == 0) st_granule(ho_r + 4 * n, ho_tag, __float_as_uint(px[ct]));
+          else if (p == 1) st_granule(ho_r + 4 * n + 1, ho_tag, __float_as_uint(py[ct]));
+          else if (p == 2) st_granule(ho_r + 4 * n + 2, ho_tag, __float_as_uint(vx[ct]));
+          else {
+            st_granule(ho_r + 4 * n + 3, ho_tag, __float_as_uint(vy[ct]));
+            st_granule(ho_r + 9 * N + n, ho_tag, (uint32_t)action[ct]);
+          }
+        }
+      }
+    }
     if (it == 0) SWARM_STAMP(5);
     // ---- env.step (VMAS World.step + scenario reward).  The 4 row groups of an agent
     //      split its partner pairs (group p: partners p, p + 4, ...), then every lane sums
@@ -259,6 +281,11 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 #pragma unroll
       for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
       o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
+      if (MODE == MODE_TICK && HO && ho_r && valid[ct]) {
+        const int nn = 16 * ct + c;
+        const float v = p == 0 ? o[ct].px : (p == 1 ? o[ct].py : (p == 2 ? o[ct].vx : o[ct].vy));
+        st_granule(ho_r + 4 * N + 4 * nn + p, ho_tag, __float_as_uint(v));
+      }
       if (16 * ct + c < NS && p == 0) { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }
     }
     if (it == 0) SWARM_STAMP(3);
@@ -284,6 +311,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const float rew = (SCEN == SWARM_GOTO) ? rg : oa_reward(o[ct].dgoal, o[ct].dobs);
+      if (MODE == MODE_TICK && HO && ho_r && valid[ct] && p == 0)
+        st_granule(ho_r + 8 * N + 16 * ct + c, ho_tag, __float_as_uint(rew));
       const int n = 16 * ct + c;
       if (valid[ct]) {   // the node's four row groups share its stores
         if (MODE == MODE_TICK || MODE == MODE_STEP) {
@@ -304,25 +333,6 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
             if (p == 1) reinterpret_cast<float4*>(rp_s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
             else if (p == 2) reinterpret_cast<float4*>(rp_sn)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
             else { rp_r[ri] = rew; rp_a[ri] = (uint8_t)action[ct]; }
-            if (HO && ho_pub) {   // tagged write-through copy for this tick's TD waves (hand-off record)
-              unsigned long long* rec = A.ho_rec + (size_t)d.gid * ho_stride_granules(N);
-              const uint32_t tag = cc.tick + 1u;
-              if (p == 1) {
-                st_granule(rec + 4 * n, tag, __float_as_uint(px[ct]));
-                st_granule(rec + 4 * n + 1, tag, __float_as_uint(py[ct]));
-                st_granule(rec + 4 * n + 2, tag, __float_as_uint(vx[ct]));
-                st_granule(rec + 4 * n + 3, tag, __float_as_uint(vy[ct]));
-              } else if (p == 2) {
-                unsigned long long* r2 = rec + 4 * N + 4 * n;
-                st_granule(r2, tag, __float_as_uint(o[ct].px));
-                st_granule(r2 + 1, tag, __float_as_uint(o[ct].py));
-                st_granule(r2 + 2, tag, __float_as_uint(o[ct].vx));
-                st_granule(r2 + 3, tag, __float_as_uint(o[ct].vy));
-              } else {
-                st_granule(rec + 8 * N + n, tag, __float_as_uint(rew));
-                st_granule(rec + 9 * N + n, tag, (uint32_t)action[ct]);
-              }
-            }
           }
           if (p == 3 && A.out.obs) {
             float* ob = A.out.obs + node[ct] * 6;

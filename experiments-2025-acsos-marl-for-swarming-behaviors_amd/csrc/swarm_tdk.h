@@ -216,7 +216,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     if (pending && (cc.tick % (uint32_t)X.hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
     else ptg.store(Ptg, threadIdx.x);
     // waves whose graphs wait for a hand-off are the tick's critical path: top issue priority
-    if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off)
+    if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off):
+                    // online waves s and a, target waves s' (r is swept before y)
       const uint32_t tag = cc.tick + 1u;
       for (int spin = 0;; ++spin) {
         bool ok = true;
@@ -228,13 +229,12 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
             const unsigned long long* sp = rec + (online ? 0 : 4 * N) + 4 * j;
             const unsigned long long g0 = ld_granule(sp), g1 = ld_granule(sp + 1), g2 = ld_granule(sp + 2),
                                      g3 = ld_granule(sp + 3);
-            const unsigned long long g4 = ld_granule(rec + (online ? 9 * N : 8 * N) + j);
+            const unsigned long long g4 = online ? ld_granule(rec + 9 * N + j) : ((unsigned long long)tag << 32);
             ok = ok && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag && (uint32_t)(g2 >> 32) == tag &&
                  (uint32_t)(g3 >> 32) == tag && (uint32_t)(g4 >> 32) == tag;
             st[ct] = make_float4(__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1),
                                  __uint_as_float((uint32_t)g2), __uint_as_float((uint32_t)g3));
             if (online) act[ct] = nv[ct] ? (int)(uint32_t)g4 : 0;
-            else rew[ct] = __uint_as_float((uint32_t)g4);
           }
         }
         if (!__builtin_amdgcn_ballot_w64(!ok)) break;
@@ -269,6 +269,27 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   //      Everything after B1 waits for the target waves' y, so they issue first.
   if (!online && !waited) __builtin_amdgcn_s_setprio(2);
   dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, A.radius, conv, nullptr, V, online, F);
+  if (FUSED && waited && !online) {   // r of this tick's transitions (published after the reward)
+    const uint32_t tag = cc.tick + 1u;
+    for (int spin = 0;; ++spin) {
+      bool ok = true;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        if (ho[ct]) {
+          const unsigned long long g = ld_granule(X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) +
+                                                  8 * N + min(jl[ct], N - 1));
+          ok = ok && (uint32_t)(g >> 32) == tag;
+          rew[ct] = __uint_as_float((uint32_t)g);
+        }
+      }
+      if (!__builtin_amdgcn_ballot_w64(!ok)) break;
+      if (spin >= kHoSpinLimit) {
+        if (lane == 0) atomicAdd(X.ho_err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   if (!online && p == 0) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {

@@ -68,10 +68,10 @@ def main():
     raw.swarm_dbg_stamps_td.argtypes = [ctypes.c_void_p]
     eng.reset(0)
     for _ in range(30):
-        eng.train_tick()
+        eng.train_tick3()
     torch.cuda.synchronize()
     assert raw.swarm_dbg_stamps_act(sa.data_ptr()) == 0 and raw.swarm_dbg_stamps_td(st.data_ptr()) == 0
-    graph = eng.capture(3, lambda: eng.train_tick(full_out=False))   # bench.py's replay path
+    graph = eng.capture(3, lambda: eng.train_tick3(full_out=False))   # the 3-launch tick (same act / TD bodies)
     graph.replay()
     torch.cuda.synchronize()
     ab = (B + 3) // 4

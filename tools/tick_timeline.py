@@ -15,6 +15,10 @@ import torch  # noqa: E402
 
 import swarm_amd  # noqa: E402
 from swarm_amd import _lib  # noqa: E402
+from tools.stamps import ACT, ACT_ORDER, TD, report  # noqa: E402
+
+TD_WAIT = {**TD, 10: "hand-off (granules matched)", 2: "B0 barrier"}
+TD_WAIT_ORDER = [0, 1, 10, 2, 16, 17, 18, 19, 20, 3, 4, 5, 24, 25, 27, 6, 7]
 
 
 def main():
@@ -60,6 +64,15 @@ def main():
             print(f"  TD block {b}: hand-off at {hw.round(2).tolist()} us, block end {us(td[b, :, 9].max()):.2f} us")
         nw = te[te > np.percentile(te, 99)]
         print(f"  slowest 1% TD waves end at {np.sort(nw).round(2).tolist()[-6:]} us")
+        if rep == 2:   # per-segment medians (s_memtime cycles) of the critical waves
+            print("  acting waves:")
+            report(act.reshape(-1), ACT, act.shape[0] * 4, ACT_ORDER)
+            wv = td.reshape(-1, 32)
+            wv = wv[wv[:, 10] > 0]
+            wv = wv[wv[:, 24] > 0]   # online waves of waiting graphs
+            if len(wv):
+                print(f"  online TD waves of hand-off graphs ({len(wv)}):")
+                report(wv.reshape(-1), TD_WAIT, len(wv), TD_WAIT_ORDER)
 
 
 if __name__ == "__main__":
