@@ -377,16 +377,20 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
     const float b1v[2][4] = {{bb0.x, bb0.y, bb0.z, bb0.w}, {bb1.x, bb1.y, bb1.z, bb1.w}};
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
+      // the two output tiles' chains interleaved (independent accumulators: 32-cycle issue
+      // instead of the 40-cycle dependent latency per MFMA); each chain keeps its k order
+      f32x4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) z[t2] = mfma16(a1[t2][t][r], F.t[ct][t][r], z[t2]);
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
-        f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) z = mfma16(a1[t2][t][r], F.t[ct][t][r], z);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float u = z[r] + b1v[t2][r];
+          const float u = z[t2][r] + b1v[t2][r];
           F.zr[ct][t2][r] = u > 0.0f ? u : 0.0f;
         }
       }

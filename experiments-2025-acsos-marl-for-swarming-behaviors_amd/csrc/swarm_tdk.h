@@ -346,18 +346,26 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c;
+      // W1 fragments first (16 LDS reads in flight), then the two output tiles' chains interleaved
+      float w1f[2][2][4];
 #pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            acc = mfma16(P[L_W1 + (16 * t + 4 * p + r) * kWRow + 16 * t2 + c], dz[ct][t][r], acc);
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          dO[ct][t2][r] = nv[ct] ? acc[r] * (1.0f - F.t[ct][t2][r] * F.t[ct][t2][r]) : 0.0f;
-      }
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) w1f[t2][t][r] = P[L_W1 + (16 * t + 4 * p + r) * kWRow + 16 * t2 + c];
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) acc[t2] = mfma16(w1f[t2][t][r], dz[ct][t][r], acc[t2]);
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dO[ct][t2][r] = nv[ct] ? acc[t2][r] * (1.0f - F.t[ct][t2][r] * F.t[ct][t2][r]) : 0.0f;
       if (n < NS) {
         *reinterpret_cast<float4*>(&TB.dO[row0 + n][4 * p]) = make_float4(dO[ct][0][0], dO[ct][0][1], dO[ct][0][2], dO[ct][0][3]);
         *reinterpret_cast<float4*>(&TB.dO[row0 + n][16 + 4 * p]) = make_float4(dO[ct][1][0], dO[ct][1][1], dO[ct][1][2], dO[ct][1][3]);
