@@ -35,16 +35,24 @@ struct TdLds {
   float H[kTdRows][kRow];         // online conv1.lin output
   float T[kTdRows][kRow];         // tanh(conv out)
   float R[kTdRows][kRow];         // relu(lin1)
+  // written only after B1; before it, rows NS w .. NS w + NS - 1 of dZ / dO / dH are target
+  // wave w's forward scratch (its H / T / R rows): 13.8 KB less LDS per block, so three
+  // 256-thread blocks fit a CU (the fused tick at N = 9..16 has 3 blocks per CU)
   float dZ[kTdRows][kRow];        // dL/d lin1 pre-activation
   float dO[kTdRows][kRow];        // dL/d conv out
   float dH[kTdRows][kRow];        // dL/d h
   float X[kTdRows][9];            // node features (k < 8)
-  float cm[kTdRows][NS + 1];      // c[target row][source slot]
-  float dp[kTdRows][NS + 1];      // dL/d pre-activation of edge (source -> target row)
+  union {
+    struct {
+      float cm[kTdRows][NS + 1];  // c[target row][source slot]
+      float dp[kTdRows][NS + 1];  // dL/d pre-activation of edge (source -> target row)
+    };
+    WSmall<NS> tgsm[GPB];         // before B1: the target waves' small scratch
+  };
   float y[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];
   int act[kTdRows];
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
-  WScratch<NS> tg[GPB];           // target waves' forward scratch
+  __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
 };
 
 struct TdArgs {
@@ -124,7 +132,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   const int graph = spec_graph<SPEC>(A.graph);
   const int conv = spec_conv<SPEC>(A.conv);
   const int row0 = wi * NS;
-  const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.tg[wi].view();
+  const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.target_view(wi);
   const int lane = d.lane, c = d.c, p = d.p;
   float* gslab = A.slabs + (size_t)vb * (N_PARAMS + 1);
   SWARM_RTSTAMP(8);
