@@ -97,6 +97,30 @@ def test_host_sample_permutation_and_inverse_match_oracle():
             assert sorted(lib.swarm_host_sample_position(g, n, k0, k1, rnd) for g in range(n)) == list(range(n))
 
 
+def test_fused_tick_support_and_workspace_host_side():
+    """swarm_train_tick's host-side contract (no GPU call): which configurations have a
+    one-launch tick, its workspace size (error word + one 128-B-aligned granule record per
+    env), and the error codes it returns before launching anything."""
+    L, lib = _host_lib()
+    def cfg(B=1024, N=8, graph=0, k=5, conv=0, radius=0.0):
+        return L.SwarmConfig(B, N, 0, graph, k, conv, 0, 0, 0, radius, 0)
+    ok = [cfg(), cfg(N=16), cfg(N=12, conv=1), cfg(graph=1, k=5), cfg(graph=3, radius=0.3), cfg(B=1, N=1)]
+    bad = [cfg(N=17), cfg(N=32), cfg(graph=2), cfg(graph=1, k=9), cfg(graph=3, radius=0.0), cfg(B=0)]
+    for c in ok:
+        assert lib.swarm_train_tick_supported(ctypes.byref(c)) == 1
+        n_gran = -(-10 * c.n_agents // 16) * 16
+        assert lib.swarm_train_tick_workspace_bytes(ctypes.byref(c)) == 128 + c.n_envs * n_gran * 8
+    for c in bad:
+        assert lib.swarm_train_tick_supported(ctypes.byref(c)) == 0
+        assert lib.swarm_train_tick_workspace_bytes(ctypes.byref(c)) == -4
+    hp = L.SwarmAdamCfg(1e-3, 0.9, 0.999, 1e-8, 1.0, 0.99, 32, 200, 1, 0)
+    lr = L.SwarmLearner(*([1] * 8))
+    rp = L.SwarmReplay(1, 1, 1, 1, 4, 0)
+    args = (ctypes.byref(hp), ctypes.byref(lr), 1, ctypes.byref(rp), 1, None, 1, 1, None, None)
+    assert lib.swarm_train_tick(ctypes.byref(bad[0]), *args) == -4
+    assert lib.swarm_train_tick(ctypes.byref(ok[0]), *args[:6], 1, None, None, None) == -1   # no workspace
+
+
 @pytest.mark.parametrize("n", [1, 5, 8, 12])
 def test_dense_forward_equals_edge_list_forward(golden_weights, n):
     params = O.unflatten_params(torch.tensor(golden_weights["go_to"][1]))
