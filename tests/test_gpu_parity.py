@@ -531,3 +531,26 @@ def test_simulator_and_trainer_smoke(sw, golden_weights, tmp_path):
     assert list(sd.keys()) == [k for k, _ in O.PARAM_ORDER]
     rows = list(csv.reader(open(tmp_path / "stats" / "experiment_GoTo-seed_0.csv")))
     assert rows[0] == ["Episode", "Reward", "Loss"] and rows[1][0] == "9"
+
+
+def test_training_curve_matches_reference_statistically(sw):
+    """Training-path parity (unpinned bit for bit): DQNTrainer.train_model
+    with the reference script's configuration (train_gcn_dqn.py:262-290; 10 agents, 1 env,
+    batch 32, target sync every 200 ticks, eps 0.99 decaying by 0.01/episode) learns GoTo along
+    the reference's recorded curves (tests/golden/train_stats.json from data/stats).  Two
+    seeds x 300 episodes here; tools/train_parity.py runs the full 10 seeds x 1000 episodes
+    (profiles/r01_train_parity.json)."""
+    import json
+    import os
+    import statistics
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from train_parity import run
+    ref = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_stats.json")))
+    curves = [run("GoTo", seed, 300) for seed in (0, 1)]
+    ours_first = statistics.mean(c[0] for c in curves)
+    ours_win = statistics.mean(statistics.mean(c[20:30]) for c in curves)       # episodes 200-299
+    ref_win = [statistics.mean(ref["curves"]["GoTo"][str(s)]["reward"][20:30]) for s in range(10)]
+    assert ours_win - ours_first > 80.0, (ours_first, ours_win)                # it learns
+    assert abs(ours_win - statistics.mean(ref_win)) < 12.0, (ours_win, statistics.mean(ref_win))
+
