@@ -554,3 +554,26 @@ def test_training_curve_matches_reference_statistically(sw):
     assert ours_win - ours_first > 80.0, (ours_first, ours_win)                # it learns
     assert abs(ours_win - statistics.mean(ref_win)) < 12.0, (ours_win, statistics.mean(ref_win))
 
+
+def test_evaluation_harness_matches_recorded_results(sw, tmp_path):
+    """The reference's evaluation harness (tests/test_*.py -> Simulator: 8 episodes, random
+    starts, kNN k = 5) over model seeds 0-9 reproduces the recorded result.csv statistics
+    (tests/golden/eval_stats.json from data/test_stats).  Starts come from Philox, not
+    torch.randn, so means are compared; tools/eval_sweep.py runs the whole agents 5-12 grid."""
+    import json
+    import os
+    import statistics
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from eval_sweep import run_one
+    here = os.path.dirname(os.path.abspath(__file__))
+    weights = np.load(os.path.join(here, "golden", "weights.npz"))
+    ref = json.load(open(os.path.join(here, "golden", "eval_stats.json")))["results"]
+    for scen, n, tol in (("obstacle_avoidance", 8, 0.05), ("go_to", 5, 0.2)):
+        ours = [r for s in range(10) for r in run_one(scen, s, n, str(tmp_path), weights)]
+        theirs = [r for s in range(10) for r in ref[scen][f"{s}/{n}"]]
+        a, b = statistics.mean(r[0] for r in ours), statistics.mean(r[0] for r in theirs)
+        assert abs(a - b) <= tol * abs(b), (scen, a, b)
+        assert (tmp_path / scen / "seed_9" / f"agents_{n}" / "positions" / "positions_episode_7_x.csv").exists()
+
