@@ -147,14 +147,13 @@ class SwarmEngine:
         self.grad = torch.zeros(N_PARAMS + 3, **f32)
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
-        # fused-tick workspace (hand-off flags, error word, records); zeroed with ctrl
+        # fused-tick workspace (error word, hand-off granule records); zeroed with ctrl
         self.fused = learn and bool(self.lib.swarm_train_tick_supported(ctypes_ref(self.cfg)))
         self.tick_ws = None
         if self.fused:
             nb = self.lib.swarm_train_tick_workspace_bytes(ctypes_ref(self.cfg))
             check(int(min(nb, 0)), "swarm_train_tick_workspace_bytes")
             self.tick_ws = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
-            self._ho_err_off = 0
         # per-tick outputs
         self.q = torch.zeros(n_envs, n_agents, 9, **f32)
         self.actions = torch.zeros(n_envs, n_agents, dtype=torch.int32, device=dev)
@@ -283,7 +282,7 @@ class SwarmEngine:
         """Hand-off waits of the fused tick that hit their bound (0 in a correct run)."""
         if self.tick_ws is None:
             return 0
-        return int(self.tick_ws[self._ho_err_off:self._ho_err_off + 4].view(torch.int32).item())
+        return int(self.tick_ws[:4].view(torch.int32).item())   # the workspace's first word
 
     def train_tick(self, full_out: bool = False):
         """Fused training tick: 2 launches (+ an RCCL all-reduce when world_size > 1), or the

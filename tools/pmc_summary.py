@@ -1,4 +1,4 @@
-"""Summarise the rocprofv3 --pmc passes of prof_pmc.sh into per-kernel medians and the
+"""Summarise the rocprofv3 --pmc passes of scripts/pmc.sh into per-kernel medians and the
 HBM traffic per launch that bench.py's roofline reports.
 
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch; on gfx950 FETCH_SIZE reports half the
@@ -25,7 +25,7 @@ def main(src, dst):
             for key, pat in KERNELS.items():
                 if pat in r["Kernel_Name"]:
                     vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    out = {"source": "rocprofv3 --kernel-trace --pmc, four separate passes (prof_pmc.sh), bench.py workload",
+    out = {"source": "rocprofv3 --kernel-trace --pmc, four separate passes (scripts/pmc.sh), bench.py workload",
            "units": "counter medians per dispatch; *_bytes in bytes",
            "kernels": {}}
     for key in KERNELS:
