@@ -47,7 +47,7 @@ def _tie_mask(q):
 
 # ------------------------------------------------------------------ env.step
 @pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
-@pytest.mark.parametrize("N", [1, 5, 8, 12, 29])
+@pytest.mark.parametrize("N", [1, 5, 8, 12, 29, 32])
 def test_env_step_parity(sw, scen, N):
     B = 96
     eng = sw.SwarmEngine(scen, N, B, seed=1, learn=False)
@@ -94,15 +94,15 @@ def test_knn_graph_bit_exact(sw, N, k):
     lib = _lib.load()
     for tight in (True, False):
         pos, vel = _rand_state(B, N, N * 31 + k, tight=tight)
-        x = O.node_features(pos, vel).reshape(B * N, 7)
+        xd = O.node_features(pos, vel).reshape(B * N, 7).cuda()
         mult = torch.zeros((B * N * N + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
         cfg = _lib.SwarmConfig(B, N, 0, _lib.GRAPH_KNN, k, 0, 0, 0, 0)
-        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
+        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), xd.data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
         got = mult[: B * N * N].view(B, N, N).cpu().float()
         ref = O.multiplicity_knn(O.knn_sets(pos, k))
         assert torch.equal(got, ref)
         cfg.graph = _lib.GRAPH_COMPLETE
-        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
+        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), xd.data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
         assert torch.equal(mult[: B * N * N].view(B, N, N).cpu().float(), O.multiplicity_complete(B, N))
 
 
@@ -117,16 +117,16 @@ def test_radius_graph_bit_exact(sw, N, radius):
     lib = _lib.load()
     for tight in (True, False):
         pos, vel = _rand_state(B, N, N * 7 + int(radius * 100), tight=tight)
-        x = O.node_features(pos, vel).reshape(B * N, 7)
+        xd = O.node_features(pos, vel).reshape(B * N, 7).cuda()
         mult = torch.zeros((B * N * N + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
         cfg = _lib.SwarmConfig(B, N, 0, _lib.GRAPH_RADIUS, 0, 0, 0, 0, 0, radius, 0)
-        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
+        _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), xd.data_ptr(), mult.data_ptr(), _lib.stream_ptr()), "g")
         got = mult[: B * N * N].view(B, N, N).cpu().float()
         ref = O.multiplicity_radius(O.radius_sets(pos, radius))
         assert torch.equal(got, ref)
         assert 0 < int((ref > 0).sum()) - B < B * N * (N - 1)   # neither empty nor complete
     cfg.radius = 0.0
-    assert lib.swarm_build_graph(ctypes.byref(cfg), x.cuda().data_ptr(), mult.data_ptr(), _lib.stream_ptr()) == -1
+    assert lib.swarm_build_graph(ctypes.byref(cfg), xd.data_ptr(), mult.data_ptr(), _lib.stream_ptr()) == -1
 
 
 def test_knn_k_larger_than_n_raises(sw):
@@ -576,4 +576,57 @@ def test_evaluation_harness_matches_recorded_results(sw, tmp_path):
         a, b = statistics.mean(r[0] for r in ours), statistics.mean(r[0] for r in theirs)
         assert abs(a - b) <= tol * abs(b), (scen, a, b)
         assert (tmp_path / scen / "seed_9" / f"agents_{n}" / "positions" / "positions_episode_7_x.csv").exists()
+
+
+def test_maximum_swarm_and_empty_inputs(sw, golden_weights):
+    """Edge sizes: the ABI's largest swarm (32 agents) through forward (complete, kNN with
+    k = N, radius), the acting tick and a TD update; a radius covering the arena gives the
+    complete graph exactly; empty batches (0 envs) are no-ops that return 0."""
+    import ctypes
+    from swarm_amd import _lib
+    lib = _lib.load()
+    B, N = 24, 32
+    p = _params(golden_weights, "obstacle_avoidance", 1)
+    pos, vel = _rand_state(B, N, 5)
+    x = O.node_features(pos, vel).reshape(B * N, 7).cuda()   # device copies kept alive across the calls
+    pd = p.cuda()
+    for graph, k, r, mult in ((_lib.GRAPH_COMPLETE, 0, 0.0, O.multiplicity_complete(B, N)),
+                              (_lib.GRAPH_KNN, N, 0.0, O.multiplicity_knn(O.knn_sets(pos, N))),
+                              (_lib.GRAPH_RADIUS, 0, 0.4, O.multiplicity_radius(O.radius_sets(pos, 0.4))),
+                              (_lib.GRAPH_RADIUS, 0, 100.0, O.multiplicity_complete(B, N))):
+        cfg = _lib.SwarmConfig(B, N, 1, graph, k, 0, 0, 0, 0, r, 0)
+        m = torch.zeros(B * N * N, dtype=torch.uint8, device="cuda")
+        if graph != _lib.GRAPH_COMPLETE:
+            _lib.check(lib.swarm_build_graph(ctypes.byref(cfg), x.data_ptr(), m.data_ptr(), _lib.stream_ptr()), "g")
+            torch.cuda.synchronize()
+            assert torch.equal(m.view(B, N, N).cpu().float(), mult)
+        q = torch.zeros(B * N, 9, device="cuda")
+        _lib.check(lib.swarm_q_forward(ctypes.byref(cfg), pd.data_ptr(), x.data_ptr(), None, q.data_ptr(),
+                                       _lib.stream_ptr()), "q")
+        torch.cuda.synchronize()
+        assert_close_rel(q.cpu().view(B, N, 9), O.q_forward_dense(O.unflatten_params(p), O.node_features(pos, vel), mult),
+                         1e-5, "Q N=32")
+    eng = sw.SwarmEngine("ObstacleAvoidance", N, B, seed=3, params=p, eps=0.3, batch=B, replay_capacity=4 * B)
+    assert not eng.fused   # n_agents > 16: the 3-launch tick
+    eng.state.copy_(torch.cat([pos, vel], -1).cuda())
+    eng.ctrl[0] = 2
+    eng.act(push=True)
+    torch.cuda.synchronize()
+    ref = O.act_tick(O.unflatten_params(p), pos, vel, O.SCENARIO_OA, O.GRAPH_COMPLETE, 0, 0.3, 3, 2)
+    clear = _tie_mask(ref.q) | ref.explore[:, None]
+    assert torch.equal(eng.actions.cpu().long()[clear], ref.actions[clear])
+    for _ in range(3):
+        eng.train_tick()
+    torch.cuda.synchronize()
+    assert eng.read_ctrl()["trained"] == 1 and np.isfinite(eng.read_ctrl()["loss"])
+    # empty batches
+    empty = _lib.SwarmConfig(0, 8, 0, _lib.GRAPH_COMPLETE, 0, 0, 0, 0, 0, 0.0, 0)
+    dummy = torch.zeros(16, device="cuda")
+    assert lib.swarm_env_reset(ctypes.byref(empty), dummy.data_ptr(), 0, _lib.stream_ptr()) == 0
+    assert lib.swarm_env_step(ctypes.byref(empty), dummy.data_ptr(), dummy.data_ptr(), None, _lib.stream_ptr()) == 0
+    assert lib.swarm_q_forward(ctypes.byref(empty), dummy.data_ptr(), dummy.data_ptr(), None, dummy.data_ptr(),
+                               _lib.stream_ptr()) == 0
+    assert lib.swarm_rollout(ctypes.byref(empty), dummy.data_ptr(), dummy.data_ptr(), 5, 0, 0.0, None,
+                             _lib.stream_ptr()) == 0
+    torch.cuda.synchronize()
 
