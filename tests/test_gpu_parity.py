@@ -438,7 +438,9 @@ def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
                                                         ("ObstacleAvoidance", 16, "gcn", 40, 2, "complete"),
                                                         ("GoTo", 8, "gcn", 1024, 977, "complete"),
                                                         ("GoTo", 8, "gat", 64, 2, "knn"),
-                                                        ("ObstacleAvoidance", 12, "gat", 48, 2, "radius")])
+                                                        ("ObstacleAvoidance", 12, "gat", 48, 2, "radius"),
+                                                        ("GoTo", 5, "gat", 37, 3, "complete"),      # ragged blocks
+                                                        ("ObstacleAvoidance", 11, "gcn", 33, 2, "knn")])
 def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, conv, B, slots, graph):
     """swarm_train_tick (acting and TD blocks in one launch, TD graphs of the tick's own slot
     read through the hand-off records) == the 3-launch tick, bit for bit, every tick.  Small
