@@ -15,12 +15,13 @@ from .engine import SwarmEngine, flatten_state_dict, unflatten_params  # noqa: F
 from .graph import (Batch, Data, create_graph_from_observations, create_knn_graph_from_observations,  # noqa: F401
                     create_radius_graph_from_observations)
 from .gcn import GCN  # noqa: F401
-from .scenarios import BaseScenario, GoToPositionScenario, ObstacleAvoidanceScenario, get_scenario  # noqa: F401
+from .scenarios import (BaseScenario, FlockingScenario, GoToPositionScenario, ObstacleAvoidanceScenario,  # noqa: F401
+                        get_scenario)
 from .env import Environment, make_env  # noqa: F401
 from .dqn import DQNTrainer, GraphReplayBuffer, set_seed  # noqa: F401
 from .simulator import Simulator  # noqa: F401
 
 __all__ = ["SwarmEngine", "Data", "Batch", "GCN", "make_env", "Environment", "GoToPositionScenario",
-           "ObstacleAvoidanceScenario", "BaseScenario", "get_scenario", "DQNTrainer", "GraphReplayBuffer",
+           "ObstacleAvoidanceScenario", "FlockingScenario", "BaseScenario", "get_scenario", "DQNTrainer", "GraphReplayBuffer",
            "set_seed", "Simulator", "create_graph_from_observations", "create_knn_graph_from_observations",
            "create_radius_graph_from_observations"]

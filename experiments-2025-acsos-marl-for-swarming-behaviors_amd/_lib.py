@@ -15,7 +15,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SWARM_LIB_PATH") or os.path.join(HERE, "libswarm_hip.so")
 
-SWARM_GOTO, SWARM_OBSTACLE_AVOIDANCE = 0, 1
+SWARM_GOTO, SWARM_OBSTACLE_AVOIDANCE, SWARM_FLOCKING = 0, 1, 2
 GRAPH_COMPLETE, GRAPH_KNN, GRAPH_DENSE, GRAPH_RADIUS = 0, 1, 2, 3
 CONV_GAT, CONV_GCN = 0, 1
 F_SHARED_RESET, F_RANDOM_OA = 1, 2
@@ -24,7 +24,7 @@ ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
           -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class SwarmConfig(ctypes.Structure):

@@ -39,6 +39,9 @@ __global__ void reset_kernel(int B, int N, int scenario, int flags, uint32_t k0,
   if (scenario == SWARM_GOTO) {
     cx = 1.5f + (-0.6f + 0.4f * z0);
     cy = -1.5f + (0.6f + 0.4f * z1);
+  } else if (scenario == SWARM_FLOCKING) {   // flocking_scenario.py:86-91: [-1, 1] + N((-0.6,0.6), 0.4)
+    cx = -1.0f + (-0.6f + 0.4f * z0);
+    cy = 1.0f + (0.6f + 0.4f * z1);
   } else {
     const float s = (flags & SWARM_F_RANDOM_OA) ? 0.1f : 0.0f;
     cx = 0.6f + s * z0;
@@ -105,7 +108,9 @@ namespace {
 
 int check_cfg(const swarm_config* c) {
   if (!c || c->n_envs < 0 || c->n_agents < 1 || c->n_agents > 32) return SWARM_E_BADARG;
-  if (c->scenario != SWARM_GOTO && c->scenario != SWARM_OBSTACLE_AVOIDANCE) return SWARM_E_BADARG;
+  if (c->scenario != SWARM_GOTO && c->scenario != SWARM_OBSTACLE_AVOIDANCE && c->scenario != SWARM_FLOCKING)
+    return SWARM_E_BADARG;
+  if (c->scenario == SWARM_FLOCKING && c->n_agents < 2) return SWARM_E_BADARG;   // mean over the other agents
   if (c->graph < 0 || c->graph > 3 || (c->conv != SWARM_CONV_GAT && c->conv != SWARM_CONV_GCN)) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_KNN && (c->knn_k < 1 || c->knn_k > c->n_agents)) return SWARM_E_KNN_K;
   if (c->graph == SWARM_GRAPH_RADIUS && !(c->radius > 0.0f)) return SWARM_E_BADARG;
@@ -145,10 +150,16 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
     else SWARM_ACT_LAUNCH1(NS, SC, SPEC_RUNTIME);                  \
   } while (0)
   constexpr int OA = (MODE == MODE_Q) ? SWARM_GOTO : SWARM_OBSTACLE_AVOIDANCE;   // MODE_Q has no physics
+  constexpr int FL = (MODE == MODE_Q) ? SWARM_GOTO : SWARM_FLOCKING;
   const bool oa = MODE != MODE_Q && a.scenario == SWARM_OBSTACLE_AVOIDANCE;
-  if (a.N <= 8) { if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO); }
-  else if (a.N <= 16) { if (oa) SWARM_ACT_LAUNCH(16, OA); else SWARM_ACT_LAUNCH(16, SWARM_GOTO); }
-  else { if (oa) SWARM_ACT_LAUNCH(32, OA); else SWARM_ACT_LAUNCH(32, SWARM_GOTO); }
+  const bool fl = MODE != MODE_Q && a.scenario == SWARM_FLOCKING;   // flocking: runtime graph/conv only
+  if (a.N <= 8) {
+    if (fl) SWARM_ACT_LAUNCH1(8, FL, SPEC_RUNTIME); else if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO);
+  } else if (a.N <= 16) {
+    if (fl) SWARM_ACT_LAUNCH1(16, FL, SPEC_RUNTIME); else if (oa) SWARM_ACT_LAUNCH(16, OA); else SWARM_ACT_LAUNCH(16, SWARM_GOTO);
+  } else {
+    if (fl) SWARM_ACT_LAUNCH1(32, FL, SPEC_RUNTIME); else if (oa) SWARM_ACT_LAUNCH(32, OA); else SWARM_ACT_LAUNCH(32, SWARM_GOTO);
+  }
 #undef SWARM_ACT_LAUNCH
 #undef SWARM_ACT_LAUNCH1
   return (int)hipGetLastError();

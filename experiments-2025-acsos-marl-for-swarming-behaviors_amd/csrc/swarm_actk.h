@@ -286,13 +286,54 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
         const float v = p == 0 ? o[ct].px : (p == 1 ? o[ct].py : (p == 2 ? o[ct].vx : o[ct].vy));
         st_granule(ho_r + 4 * N + 4 * nn + p, ho_tag, __float_as_uint(v));
       }
-      if (16 * ct + c < NS && p == 0) { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }
+      if (16 * ct + c < NS && p == 0) {
+        if (SCEN == SWARM_FLOCKING) { sm.aux[16 * ct + c] = o[ct].px; sm.aux2[16 * ct + c] = o[ct].py; }
+        else { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }
+      }
     }
     if (it == 0) SWARM_STAMP(3);
     wave_lds_sync();
+    float rf = 0.0f;   // flocking: the collective reward
+    if (SCEN == SWARM_FLOCKING) {
+      // every agent's term from its pre-step (sm.px/py) and post-step (sm.aux/aux2) distances;
+      // the scenario's "previous" values are exactly the pre-step ones (flocking_scenario.py:102-122, 140-142, 163-164)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int n = 16 * ct + c;
+        if (n < NS && p == 0) {
+          const float dpre = norm2(px[ct] - kGoalX, py[ct] - kGoalY);
+          float spre = 0.0f, spost = 0.0f, cnt = 0.0f;
+          for (int j = 0; j < N; ++j) {
+            if (j == n) continue;
+            const float a = norm2(px[ct] - sm.px[j], py[ct] - sm.py[j]) - kFlockDesired;
+            const float bn = norm2(o[ct].px - sm.aux[j], o[ct].py - sm.aux2[j]);
+            const float b = bn - kFlockDesired;
+            spre = spre + a * a;
+            spost = spost + b * b;
+            if ((bn - kRadius) - kRadius <= kFlockContact) cnt = cnt + 1.0f;   // World.get_distance
+          }
+          const float others = (float)(N - 1);   // torch mean over the N - 1 other agents
+          const float d_pre = (spre / others) * kFlockShaping, d_post = (spost / others) * kFlockShaping;
+          float rg = dpre * kFlockShaping - o[ct].dgoal * kFlockShaping;               // :140-141
+          if (o[ct].dgoal < kRadius) rg = rg + kFlockGoalBonus;                      // on_goal :138, 146-147
+          const float term = (rg + (-cnt)) + (d_pre - d_post);                       // :128-129
+          fb[n] = (n < N) ? term : 0.0f;
+          fb[NS + n] = cnt;
+          fb[2 * NS + n] = o[ct].dgoal;
+        }
+      }
+      wave_lds_sync();
+      rf = fb[0];
+#pragma unroll
+      for (int j = 1; j < NS; ++j)
+        if (j < N) rf = rf + fb[j];
+    }
     float dj[NS], hj[NS];
 #pragma unroll
-    for (int j = 0; j < NS; ++j) { dj[j] = sm.aux[j < N ? j : 0]; hj[j] = sm.aux2[j < N ? j : 0]; }
+    for (int j = 0; j < NS; ++j) {
+      if (SCEN == SWARM_FLOCKING) { dj[j] = fb[2 * NS + (j < N ? j : 0)]; hj[j] = fb[NS + (j < N ? j : 0)]; }
+      else { dj[j] = sm.aux[j < N ? j : 0]; hj[j] = sm.aux2[j < N ? j : 0]; }
+    }
     float dsum = dj[0], hsum = hj[0];
 #pragma unroll
     for (int j = 1; j < NS; ++j)
@@ -310,7 +351,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const float rew = (SCEN == SWARM_GOTO) ? rg : oa_reward(o[ct].dgoal, o[ct].dobs);
+      const float rew = (SCEN == SWARM_GOTO) ? rg : (SCEN == SWARM_FLOCKING ? rf : oa_reward(o[ct].dgoal, o[ct].dobs));
       if (MODE == MODE_TICK && HO && ho_r && valid[ct] && p == 0)
         st_granule(ho_r + 8 * N + 16 * ct + c, ho_tag, __float_as_uint(rew));
       const int n = 16 * ct + c;

@@ -28,6 +28,11 @@ constexpr float kMinDist = 1e-6f;                   // VMAS _get_constraint_forc
 constexpr float kDt = 0.1f;                         // VMAS dt (substeps = 1)
 constexpr float kDragKeep = 0.75f;                  // 1 - drag(0.25)
 constexpr float kLeakySlope = 0.2f;                 // GATConv negative_slope
+// flocking_scenario.py:10-21: shaping factors, desired spacing, contact threshold, goal bonus
+constexpr float kFlockShaping = 10.0f;              // pos_shaping_factor == dist_shaping_factor
+constexpr float kFlockDesired = 0.15f;              // desired_distance
+constexpr float kFlockContact = 0.005f;             // min_collision_distance
+constexpr float kFlockGoalBonus = 50.0f;            // distance_to_goal_reward :146-147
 
 // flat parameter layout == GCN.state_dict() order (see oracle PARAM_ORDER)
 constexpr int OFF_ATT_SRC = 0;       // [32]

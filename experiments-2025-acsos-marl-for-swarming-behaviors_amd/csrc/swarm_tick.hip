@@ -58,7 +58,8 @@ int swarm_train_tick_supported(const swarm_config* cfg) {
   if (cfg->graph == SWARM_GRAPH_RADIUS && !(cfg->radius > 0.0f)) return 0;
   return (cfg->graph == SWARM_GRAPH_COMPLETE || cfg->graph == SWARM_GRAPH_KNN || cfg->graph == SWARM_GRAPH_RADIUS) &&
          (cfg->conv == SWARM_CONV_GAT || cfg->conv == SWARM_CONV_GCN) &&
-         (cfg->scenario == SWARM_GOTO || cfg->scenario == SWARM_OBSTACLE_AVOIDANCE);
+         (cfg->scenario == SWARM_GOTO || cfg->scenario == SWARM_OBSTACLE_AVOIDANCE ||
+          (cfg->scenario == SWARM_FLOCKING && cfg->n_agents >= 2));
 }
 
 int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg) {
@@ -117,11 +118,14 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
     else if (spec == SPEC_COMPLETE_GCN) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GCN); \
     else SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_RUNTIME);                                 \
   } while (0)
+  const bool fl = cfg->scenario == SWARM_FLOCKING;   // flocking: the runtime-switched kernel only
   if (N <= 8) {
-    if (oa) SWARM_TICK_LAUNCH2(8, 8, SWARM_OBSTACLE_AVOIDANCE);
+    if (fl) SWARM_TICK_LAUNCH(8, 8, SWARM_FLOCKING, SPEC_RUNTIME);
+    else if (oa) SWARM_TICK_LAUNCH2(8, 8, SWARM_OBSTACLE_AVOIDANCE);
     else SWARM_TICK_LAUNCH2(8, 8, SWARM_GOTO);
   } else {
-    if (oa) SWARM_TICK_LAUNCH2(16, 16, SWARM_OBSTACLE_AVOIDANCE);
+    if (fl) SWARM_TICK_LAUNCH(16, 16, SWARM_FLOCKING, SPEC_RUNTIME);
+    else if (oa) SWARM_TICK_LAUNCH2(16, 16, SWARM_OBSTACLE_AVOIDANCE);
     else SWARM_TICK_LAUNCH2(16, 16, SWARM_GOTO);
   }
 #undef SWARM_TICK_LAUNCH2

@@ -39,7 +39,8 @@ from ._lib import (CTRL, N_PARAMS, SwarmActOut, SwarmAdamCfg, SwarmConfig, Swarm
                    stream_ptr)
 
 SCENARIOS = {"GoTo": _lib.SWARM_GOTO, "ObstacleAvoidance": _lib.SWARM_OBSTACLE_AVOIDANCE,
-             "go_to": _lib.SWARM_GOTO, "obstacle_avoidance": _lib.SWARM_OBSTACLE_AVOIDANCE}
+             "Flocking": _lib.SWARM_FLOCKING, "go_to": _lib.SWARM_GOTO,
+             "obstacle_avoidance": _lib.SWARM_OBSTACLE_AVOIDANCE, "flocking": _lib.SWARM_FLOCKING}
 GRAPHS = {"complete": _lib.GRAPH_COMPLETE, "knn": _lib.GRAPH_KNN, "radius": _lib.GRAPH_RADIUS}
 CONVS = {"gat": _lib.CONV_GAT, "gcn": _lib.CONV_GCN}
 

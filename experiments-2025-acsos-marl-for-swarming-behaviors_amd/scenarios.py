@@ -2,7 +2,8 @@
 
 In the reference these are VMAS ``BaseScenario`` subclasses whose
 ``reset_world_at`` / ``reward`` / ``observation`` VMAS calls on every step
-(src/scenarios/go_to_position_scenario.py, src/scenarios/obstacle_avoidance_scenario.py).
+(src/scenarios/go_to_position_scenario.py, src/scenarios/obstacle_avoidance_scenario.py,
+src/scenarios/flocking_scenario.py).
 Here the arithmetic of those methods lives in the HIP kernels
 (``csrc/swarm_env.h`` agent_step / oa_reward, ``csrc/swarm_act.hip`` reset);
 the classes carry the configuration and expose the metric helpers the
@@ -112,10 +113,48 @@ class ObstacleAvoidanceScenario(BaseScenario):
         return d.mean()
 
 
+class FlockingScenario(BaseScenario):
+    """flocking_scenario.py: goal (-0.8, 0.8); collective reward, summed over agents, of the
+    shaped goal progress (x10, +50 on the goal), -1 per agent in contact
+    (World.get_distance <= 0.005) and the shaped change of the mean squared deviation
+    from the desired spacing 0.15 (x10); reset centre [-1, 1] + N((-0.6,0.6), 0.4)
+    shared by every env (:9-176).  The kernel holds the scenario's constants, so only
+    the reference's defaults are accepted."""
+
+    SCENARIO_ID = _lib.SWARM_FLOCKING
+
+    def make_world(self, batch_dim, device, **kwargs):
+        super().make_world(batch_dim, device, **kwargs)
+        self.pos_shaping_factor = kwargs.get("pos_shaping_factor", 10.0)
+        self.dist_shaping_factor = kwargs.get("dist_shaping_factor", 10.0)
+        self.agent_radius = kwargs.get("agent_radius", 0.1)   # unused by the physics (VMAS sphere r=0.05)
+        if self.pos_shaping_factor != 10.0 or self.dist_shaping_factor != 10.0:
+            raise NotImplementedError("FlockingScenario: the kernels hold the reference's shaping factors (10, 10)")
+        if self.n_agents < 2:
+            raise ValueError("FlockingScenario needs n_agents >= 2 (its spacing reward averages over the others)")
+        self.desired_distance = 0.15
+        self.min_collision_distance = 0.005
+        self.agent_collision_reward = -1
+        self.random = True
+        return self
+
+    def distance_to_goal_all(self):
+        """flocking_scenario.py:188-195: [B, N] distances to the goal."""
+        pos = self.env.engine.state[..., :2]
+        return torch.linalg.vector_norm(pos - torch.tensor(GOAL, device=pos.device), dim=-1)
+
+    def agent_contacts(self):
+        """Agents in contact after the last step, summed over agents and envs (the count
+        behind the scenario's -1 avoidance terms)."""
+        return self.env.engine.hits.sum()
+
+
 def get_scenario(experiment_name: str) -> BaseScenario:
-    """train_gcn_dqn.py:241-249 (Flocking is out of scope: SURVEY §2)."""
+    """train_gcn_dqn.py:241-249."""
     if experiment_name == "GoTo":
         return GoToPositionScenario()
     if experiment_name == "ObstacleAvoidance":
         return ObstacleAvoidanceScenario()
+    if experiment_name == "Flocking":
+        return FlockingScenario()
     raise Exception(f"Scenario {experiment_name} not supported! Please check :)")

@@ -22,14 +22,16 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 4
+#define SWARM_ABI_VERSION 5
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
 #define SWARM_E_NOGPU (-3)
 #define SWARM_E_UNSUPPORTED (-4) /* configuration has no fused-tick kernel (use the 3-launch tick) */
 
-enum swarm_scenario { SWARM_GOTO = 0, SWARM_OBSTACLE_AVOIDANCE = 1 };
+/* SWARM_FLOCKING: src/scenarios/flocking_scenario.py (the reference's third scenario class,
+   train_gcn_dqn.py:244-245); needs n_agents >= 2 */
+enum swarm_scenario { SWARM_GOTO = 0, SWARM_OBSTACLE_AVOIDANCE = 1, SWARM_FLOCKING = 2 };
 enum swarm_graph { SWARM_GRAPH_COMPLETE = 0, SWARM_GRAPH_KNN = 1, SWARM_GRAPH_DENSE = 2, SWARM_GRAPH_RADIUS = 3 };
 enum swarm_conv { SWARM_CONV_GAT = 0, SWARM_CONV_GCN = 1 };
 

@@ -14,6 +14,9 @@ What it restates (citations relative to the reference checkout):
   drag + Euler integration, then the scenario ``reward`` / ``observation``.
 * ``GoToPositionScenario`` (``src/scenarios/go_to_position_scenario.py:52-143``).
 * ``ObstacleAvoidanceScenario`` (``src/scenarios/obstacle_avoidance_scenario.py:63-173``).
+* ``FlockingScenario`` (``src/scenarios/flocking_scenario.py:9-176``): reset centre and the
+  shaped collective reward (``flocking_reward``).  Parity unpinned: the reference holds no
+  Flocking trajectories (its ``data/test_stats`` cover GoTo and ObstacleAvoidance only).
 * PyG 2.5.3 ``GATConv`` (heads=1, add_self_loops=False, negative_slope=0.2, bias)
   and ``torch_geometric.utils.softmax`` (third-party, ``requirements.txt:2``).
 * ``GCN.forward`` (``src/training/train_gcn_dqn.py:59-70``).
@@ -52,6 +55,10 @@ MIN_DIST = 1e-6                 # VMAS _get_constraint_forces min_dist
 DT = 0.1                        # VMAS World dt, substeps=1
 DRAG = 0.25                     # VMAS World drag default
 GRID_SPACING = 0.15             # desired_distance (go_to_position_scenario.py:17)
+FLOCK_SHAPING = 10.0            # flocking_scenario.py:10-11 pos/dist_shaping_factor
+FLOCK_DESIRED = 0.15            # flocking_scenario.py:20 desired_distance
+FLOCK_CONTACT = 0.005           # flocking_scenario.py:21 min_collision_distance
+FLOCK_GOAL_BONUS = 50.0         # flocking_scenario.py:146-147
 N_ACTIONS = 9
 N_FEATURES = 7
 HIDDEN = 32
@@ -59,6 +66,7 @@ ACTION_LEVELS = (0.0, -1.0, 1.0)  # discrete level index -> u component (SURVEY 
 
 SCENARIO_GOTO = 0
 SCENARIO_OA = 1
+SCENARIO_FLOCK = 2
 
 PARAM_ORDER = (  # == GCN.parameters() order / state_dict order (PyG registers att, bias, then lin)
     ("conv1.att_src", (1, 1, HIDDEN)),
@@ -154,7 +162,10 @@ def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenar
     pos_new = pos + vel_new * DT
     goal = f32(GOAL)
     dist_goal = vector_norm2(pos_new - goal)                    # [B, N]
-    if scenario == SCENARIO_GOTO:
+    if scenario == SCENARIO_FLOCK:
+        rew, hits = flocking_reward(pos, pos_new)
+        d_obs = torch.zeros(B, N)
+    elif scenario == SCENARIO_GOTO:
         r = torch.zeros(B)
         acc = None
         for j in range(N):                                      # go_to_position_scenario.py:108-115
@@ -170,6 +181,54 @@ def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenar
     avg_dist = torch.mean(dist_goal, dim=1)
     return dict(pos=pos_new, vel=vel_new, force=force, rew=rew, dist_goal=dist_goal,
                 avg_dist=avg_dist, hits=hits, d_obs=d_obs)
+
+
+def _flock_agent_spread(pos: torch.Tensor, i: int) -> torch.Tensor:
+    """flocking_scenario.py:151-162 (and :110-122): mean over the other agents of
+    (|p_i - p_j| - desired)^2, times dist_shaping_factor."""
+    N = pos.shape[1]
+    d = torch.stack([vector_norm2(pos[:, i] - pos[:, j]) for j in range(N) if j != i], dim=1)
+    return (d - FLOCK_DESIRED).pow(2).mean(-1) * FLOCK_SHAPING
+
+
+def flocking_reward(pos: torch.Tensor, pos_new: torch.Tensor):
+    """FlockingScenario.reward (flocking_scenario.py:124-176) for [B, N] agents.
+
+    The scenario keeps ``previous_distance_to_goal`` / ``previous_distance_to_agents``
+    per agent; both are exactly the shaped values of the pre-step positions (set at reset,
+    :102-122, and by the previous step's reward), so they are recomputed from ``pos``.
+    ``if agent.on_goal`` only works at B=1 in the reference; this is its batched form.
+    Returns (collective reward broadcast to [B, N], contact count per env)."""
+    B, N, _ = pos.shape
+    goal = f32(GOAL)
+    total, contacts = None, torch.zeros(B)
+    for i in range(N):
+        d_now = vector_norm2(pos_new[:, i] - goal)
+        pos_rew = vector_norm2(pos[:, i] - goal) * FLOCK_SHAPING - d_now * FLOCK_SHAPING
+        r_goal = torch.where(d_now < SPHERE_RADIUS, pos_rew + FLOCK_GOAL_BONUS, pos_rew)
+        cnt = torch.zeros(B)
+        for j in range(N):
+            if j != i:   # World.get_distance(agent, other) <= min_collision_distance
+                gd = (vector_norm2(pos_new[:, i] - pos_new[:, j]) - SPHERE_RADIUS) - SPHERE_RADIUS
+                cnt = cnt + (gd <= FLOCK_CONTACT).to(torch.float32)
+        dist_rew = _flock_agent_spread(pos, i) - _flock_agent_spread(pos_new, i)
+        term = (r_goal + (-cnt)) + dist_rew
+        total = term if total is None else total + term
+        contacts = contacts + cnt
+    return total.unsqueeze(1).expand(B, N).clone(), contacts
+
+
+def flocking_reward_scale(pos: torch.Tensor, pos_new: torch.Tensor) -> torch.Tensor:
+    """[B] sum of the magnitudes the flocking reward is a difference of (shaped goal distances
+    and spreads, before and after the step).  The reward cancels most of it, so its fp32
+    rounding is bounded relative to this scale, not to the reward itself."""
+    goal = f32(GOAL)
+    N = pos.shape[1]
+    s = torch.zeros(pos.shape[0], dtype=torch.float64)
+    for i in range(N):
+        for p in (pos, pos_new):
+            s += (vector_norm2(p[:, i] - goal) * FLOCK_SHAPING).double() + _flock_agent_spread(p, i).double()
+    return s
 
 
 # ---------------------------------------------------------------------------
@@ -209,7 +268,10 @@ def reset_centres(scenario: int, n_envs: int, seed: int, episode: int, shared: b
     u2 = (w[1] >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
     rr = np.sqrt(-2.0 * np.log(u1))
     z0, z1 = rr * np.cos(2 * np.pi * u2), rr * np.sin(2 * np.pi * u2)
-    if scenario == SCENARIO_GOTO:   # (1.5,-1.5) + N((-0.6,0.6), 0.4)
+    if scenario == SCENARIO_FLOCK:  # flocking_scenario.py:86-91: [-1, 1] + N((-0.6,0.6), 0.4)
+        cx = np.float32(-1.0) + (np.float32(-0.6) + np.float32(0.4) * z0.astype(np.float32))
+        cy = np.float32(1.0) + (np.float32(0.6) + np.float32(0.4) * z1.astype(np.float32))
+    elif scenario == SCENARIO_GOTO:   # (1.5,-1.5) + N((-0.6,0.6), 0.4)
         cx = np.float32(1.5) + (np.float32(-0.6) + np.float32(0.4) * z0.astype(np.float32))
         cy = np.float32(-1.5) + (np.float32(0.6) + np.float32(0.4) * z1.astype(np.float32))
     else:                           # (0.6,-0.6) + (random ? N(0,0.1) : 0)

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     for n in sorted(names):
         assert hasattr(raw, n), n
     assert names == set(L.EXPORTED)
-    assert lib.swarm_abi_version() == 4 and lib.swarm_n_params() == O.N_PARAMS
+    assert lib.swarm_abi_version() == 5 and lib.swarm_n_params() == O.N_PARAMS
 
 
 def test_topk_emulation_matches_torch_fixture():
@@ -102,10 +102,12 @@ def test_fused_tick_support_and_workspace_host_side():
     one-launch tick, its workspace size (error word + one 128-B-aligned granule record per
     env), and the error codes it returns before launching anything."""
     L, lib = _host_lib()
-    def cfg(B=1024, N=8, graph=0, k=5, conv=0, radius=0.0):
-        return L.SwarmConfig(B, N, 0, graph, k, conv, 0, 0, 0, radius, 0)
-    ok = [cfg(), cfg(N=16), cfg(N=12, conv=1), cfg(graph=1, k=5), cfg(graph=3, radius=0.3), cfg(B=1, N=1)]
-    bad = [cfg(N=17), cfg(N=32), cfg(graph=2), cfg(graph=1, k=9), cfg(graph=3, radius=0.0), cfg(B=0)]
+    def cfg(B=1024, N=8, graph=0, k=5, conv=0, radius=0.0, scen=0):
+        return L.SwarmConfig(B, N, scen, graph, k, conv, 0, 0, 0, radius, 0)
+    ok = [cfg(), cfg(N=16), cfg(N=12, conv=1), cfg(graph=1, k=5), cfg(graph=3, radius=0.3), cfg(B=1, N=1),
+          cfg(scen=1), cfg(scen=2, N=2), cfg(scen=2, N=12, graph=1, k=5)]
+    bad = [cfg(N=17), cfg(N=32), cfg(graph=2), cfg(graph=1, k=9), cfg(graph=3, radius=0.0), cfg(B=0),
+           cfg(scen=2, N=1), cfg(scen=3)]
     for c in ok:
         assert lib.swarm_train_tick_supported(ctypes.byref(c)) == 1
         n_gran = -(-10 * c.n_agents // 16) * 16

@@ -1,0 +1,86 @@
+"""Flocking scenario (src/scenarios/flocking_scenario.py) in the oracle: the stateless
+restatement (``flocking_reward`` recomputes the scenario's "previous" values from the
+pre-step positions) against a stateful restatement that keeps them per agent exactly as the
+scenario does (:102-122 at reset, :140-142 / :163-164 on every reward call), over rollouts.
+Parity unpinned against the reference itself: it records no Flocking trajectories."""
+import math
+
+import torch
+
+from oracle import swarm_oracle as O
+
+
+class _StatefulFlocking:
+    """The scenario's reward() call sequence with its per-agent state (B envs at once;
+    ``if agent.on_goal`` written as a where)."""
+
+    def __init__(self, pos):
+        self.N = pos.shape[1]
+        goal = O.f32(O.GOAL)
+        self.prev_goal = [torch.linalg.vector_norm(pos[:, i] - goal, dim=1) * 10.0 for i in range(self.N)]
+        self.prev_agents = [self._spread(pos, i) for i in range(self.N)]
+
+    def _spread(self, pos, i):
+        d = torch.stack([torch.linalg.vector_norm(pos[:, i] - pos[:, j], dim=-1)
+                         for j in range(self.N) if j != i], dim=1)
+        return (d - 0.15).pow(2).mean(-1) * 10.0
+
+    def reward(self, pos):
+        goal = O.f32(O.GOAL)
+        collective = 0
+        for i in range(self.N):
+            d = torch.linalg.vector_norm(pos[:, i] - goal, dim=-1)
+            shaped = d * 10.0
+            r = self.prev_goal[i] - shaped
+            self.prev_goal[i] = shaped
+            r = torch.where(d < 0.05, r + 50, r)
+            avoid = torch.zeros(pos.shape[0])
+            for j in range(self.N):
+                if j != i:
+                    gd = (torch.linalg.vector_norm(pos[:, i] - pos[:, j], dim=-1) - 0.05) - 0.05
+                    avoid = avoid + torch.where(gd <= 0.005, -1.0, 0.0)
+            now = self._spread(pos, i)
+            dist_rew = self.prev_agents[i] - now
+            self.prev_agents[i] = now
+            collective = collective + ((r + avoid) + dist_rew)
+        return collective
+
+
+def _rollout(N, B, T, seed):
+    g = torch.Generator().manual_seed(seed)
+    c = O.reset_centres(O.SCENARIO_FLOCK, B, seed, 0, shared=False)
+    pos = O.grid_positions(c, N)
+    pos = pos + torch.randn(pos.shape, generator=g) * 0.02
+    vel = torch.zeros(B, N, 2)
+    ref = _StatefulFlocking(pos)
+    for t in range(T):
+        acts = torch.randint(0, 9, (B, N), generator=g)
+        out = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK)
+        want = ref.reward(out["pos"])
+        assert torch.allclose(out["rew"][:, 0], want, rtol=0, atol=2e-5), (N, t)
+        assert torch.equal(out["rew"][:, 0], out["rew"][:, -1])
+        pos, vel = out["pos"], out["vel"]
+    return out
+
+
+def test_stateless_reward_equals_stateful_scenario():
+    for N, B, T in ((2, 16, 30), (5, 32, 40), (8, 16, 25), (12, 8, 15)):
+        _rollout(N, B, T, seed=N)
+
+
+def test_goal_bonus_and_contacts():
+    # two agents: one sitting on the goal, the other touching it (|d| = 0.1 <= 0.105)
+    goal = O.f32(O.GOAL)
+    pos = torch.stack([goal, goal + torch.tensor([0.1, 0.0])])[None]
+    vel = torch.zeros(1, 2, 2)
+    out = O.env_step(pos, vel, torch.zeros(1, 2, dtype=torch.long), O.SCENARIO_FLOCK)
+    assert out["hits"].item() == 2.0                         # one contact, counted by each agent
+    # goal bonus for agent 0 only; contacts -1 each; positions change by the collision force
+    assert out["rew"][0, 0].item() > 40.0
+
+
+def test_reset_centre_distribution():
+    c = O.reset_centres(O.SCENARIO_FLOCK, 4096, 3, 0, shared=False)
+    mean = c.double().mean(0)
+    assert math.isclose(mean[0].item(), -1.6, abs_tol=0.03) and math.isclose(mean[1].item(), 1.6, abs_tol=0.03)
+    assert math.isclose(c.double().std(0)[0].item(), 0.4, abs_tol=0.03)
