@@ -20,6 +20,8 @@ GRAPH_COMPLETE, GRAPH_KNN, GRAPH_DENSE, GRAPH_RADIUS = 0, 1, 2, 3
 CONV_GAT, CONV_GCN = 0, 1
 F_SHARED_RESET, F_RANDOM_OA = 1, 2
 N_PARAMS = 1673
+NET_GCN, NET_GAT3 = 0, 1
+GAT3_N_PARAMS = 409
 ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
@@ -30,7 +32,7 @@ ABI_VERSION = 5
 class SwarmConfig(ctypes.Structure):
     _fields_ = [("n_envs", c_int32), ("n_agents", c_int32), ("scenario", c_int32), ("graph", c_int32),
                 ("knn_k", c_int32), ("conv", c_int32), ("env_offset", c_int32), ("flags", c_int32),
-                ("seed", c_uint64), ("radius", c_float), ("pad", c_int32)]
+                ("seed", c_uint64), ("radius", c_float), ("net", c_int32)]
 
 
 class SwarmReplay(ctypes.Structure):

@@ -13,13 +13,13 @@ namespace swarm {
 
 // One acting block = kActWPB environments (swarm_actk.h); the first round trip's pointers and
 // the geometry lead the parameter list (kernarg preload into SGPRs).
-template <int NS, int MODE, int SCEN, int SPEC>
+template <int NS, int MODE, int SCEN, int SPEC, int NET = SWARM_NET_GCN>
 __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
                                                           const float* grad, const float* w_cur,
                                                           const float* m_cur, const float* v_cur, int B, int N,
                                                           ActArgs A) {
   __shared__ ActSmem<NS> S;
-  act_body<NS, MODE, SCEN, SPEC>(S, blockIdx.x, gridDim.x, ctrl, state, grad, w_cur, m_cur, v_cur, B, N, A);
+  act_body<NS, MODE, SCEN, SPEC, false, NET>(S, blockIdx.x, gridDim.x, ctrl, state, grad, w_cur, m_cur, v_cur, B, N, A);
 }
 
 // ---------------------------------------------------------------- reset
@@ -111,6 +111,7 @@ int check_cfg(const swarm_config* c) {
   if (c->scenario != SWARM_GOTO && c->scenario != SWARM_OBSTACLE_AVOIDANCE && c->scenario != SWARM_FLOCKING)
     return SWARM_E_BADARG;
   if (c->scenario == SWARM_FLOCKING && c->n_agents < 2) return SWARM_E_BADARG;   // mean over the other agents
+  if (c->net != SWARM_NET_GCN && (c->net != SWARM_NET_GAT3 || c->conv != SWARM_CONV_GAT)) return SWARM_E_BADARG;
   if (c->graph < 0 || c->graph > 3 || (c->conv != SWARM_CONV_GAT && c->conv != SWARM_CONV_GCN)) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_KNN && (c->knn_k < 1 || c->knn_k > c->n_agents)) return SWARM_E_KNN_K;
   if (c->graph == SWARM_GRAPH_RADIUS && !(c->radius > 0.0f)) return SWARM_E_BADARG;
@@ -123,6 +124,7 @@ ActArgs make_args(const swarm_config* c) {
   a.k = c->knn_k; a.conv = c->conv; a.env_offset = c->env_offset; a.flags = c->flags;
   a.k0 = (uint32_t)(c->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(c->seed >> 32);
   a.radius = c->radius;
+  a.net = c->net;
   return a;
 }
 
@@ -153,6 +155,24 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   constexpr int FL = (MODE == MODE_Q) ? SWARM_GOTO : SWARM_FLOCKING;
   const bool oa = MODE != MODE_Q && a.scenario == SWARM_OBSTACLE_AVOIDANCE;
   const bool fl = MODE != MODE_Q && a.scenario == SWARM_FLOCKING;   // flocking: runtime graph/conv only
+  if constexpr (MODE != MODE_STEP) {
+  if (a.net == SWARM_NET_GAT3) {   // three-layer GAT (forward only): runtime graph
+#define SWARM_ACT_LAUNCH3(NS)                                                                                   \
+  do {                                                                                                          \
+    if (fl) hipLaunchKernelGGL((act_kernel<NS, MODE, FL, SPEC_RUNTIME, SWARM_NET_GAT3>), grid, block, 0, st,   \
+                               a.ctrl, a.state, g, w, m, v, a.B, a.N, a);                                      \
+    else if (oa) hipLaunchKernelGGL((act_kernel<NS, MODE, OA, SPEC_RUNTIME, SWARM_NET_GAT3>), grid, block, 0, \
+                                    st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a);                             \
+    else hipLaunchKernelGGL((act_kernel<NS, MODE, SWARM_GOTO, SPEC_RUNTIME, SWARM_NET_GAT3>), grid, block, 0, \
+                            st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a);                                     \
+  } while (0)
+    if (a.N <= 8) SWARM_ACT_LAUNCH3(8);
+    else if (a.N <= 16) SWARM_ACT_LAUNCH3(16);
+    else SWARM_ACT_LAUNCH3(32);
+#undef SWARM_ACT_LAUNCH3
+    return (int)hipGetLastError();
+  }
+  }
   if (a.N <= 8) {
     if (fl) SWARM_ACT_LAUNCH1(8, FL, SPEC_RUNTIME); else if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO);
   } else if (a.N <= 16) {
@@ -247,6 +267,7 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   if (int e = check_cfg(cfg)) return e;
   if (!ctrl || !hp || !lr || cfg->graph == SWARM_GRAPH_DENSE || hp->world_size < 1 || hp->update_target_every < 1)
     return SWARM_E_BADARG;
+  if (cfg->net != SWARM_NET_GCN) return SWARM_E_UNSUPPORTED;   // GAT3: forward only
   ActArgs a = make_args(cfg);
   a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = sample_out;
   static const bool no_gn = getenv("SWARM_NO_GN") != nullptr;   // A/B knob (diagnostics)

@@ -10,6 +10,7 @@
 #include "swarm_adam.h"
 #include "swarm_env.h"
 #include "swarm_dl.h"
+#include "swarm_gat3.h"
 
 namespace swarm {
 
@@ -19,6 +20,7 @@ struct ActArgs {
   int B, N, scenario, graph, k, conv, env_offset, flags;
   uint32_t k0, k1;
   float radius;            // SWARM_GRAPH_RADIUS
+  int net;                 // swarm_net (fills the padding before params: layout otherwise unchanged)
   const float* params;
   const float* x;          // MODE_Q node features [B*N][7]
   const uint8_t* dense;    // SWARM_GRAPH_DENSE multiplicity
@@ -59,8 +61,9 @@ struct ActSmem {
 
 // vb / nvb: this block's index among the nvb acting blocks of the launch (the fused
 // training-tick kernel runs acting blocks beside TD blocks).
-// HO: fused-tick hand-off publishing (swarm_tick.hip only)
-template <int NS, int MODE, int SCEN, int SPEC, bool HO = false>
+// HO: fused-tick hand-off publishing (swarm_tick.hip only).  NET: SWARM_NET_GCN (the D-layout
+// MFMA forward) or SWARM_NET_GAT3 (swarm_gat3.h; acting only, no learner prologue)
+template <int NS, int MODE, int SCEN, int SPEC, bool HO = false, int NET = SWARM_NET_GCN>
 __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int nvb,
                                          const swarm_ctrl* __restrict__ ctrl, float* state, const float* grad,
                                          const float* w_cur, const float* m_cur, const float* v_cur, int B, int N,
@@ -140,7 +143,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 #if SWARM_PIN
   asm volatile("" : "+s"(rp_s), "+s"(rp_sn), "+s"(rp_r), "+s"(rp_a), "+s"(o_rew), "+s"(o_avg), "+s"(o_hits), "+s"(smp));
 #endif
-  if (MODE == MODE_TICK && A.learn) {
+  if (MODE == MODE_TICK && NET == SWARM_NET_GCN && A.learn) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
     const int tid = threadIdx.x;
@@ -161,6 +164,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       if (pending && (tnow % (uint32_t)A.hp.update_target_every) == 0u) store4(A.lr.target, R.w, R.wt, tid);
       if (pending && tid == 0 && A.grad_norm_out) *A.grad_norm_out = gn;
     }
+  } else if (MODE != MODE_STEP && NET == SWARM_NET_GAT3) {
+    for (int i = threadIdx.x; i < G3_N_PARAMS; i += 64 * kActWPB) Pw[i] = A.params[i];
   } else if (MODE != MODE_STEP) {
     ParamStage<64 * kActWPB> ps;
     ps.load(A.params, threadIdx.x);
@@ -185,7 +190,9 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
         if (!valid[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
       }
     }
-    if (MODE != MODE_STEP) {
+    if (MODE != MODE_STEP && NET == SWARM_NET_GAT3) {
+      gat3_forward<NS>(P, d, N, graph, A.k, A.radius, A.dense, V, F);
+    } else if (MODE != MODE_STEP) {
       dl_forward<NS, 8>(P, d, N, graph, A.k, A.radius, conv, A.dense, V, false, F);
     } else {
 #pragma unroll

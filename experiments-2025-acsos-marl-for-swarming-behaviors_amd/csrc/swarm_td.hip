@@ -251,6 +251,7 @@ int check_td(const swarm_config* c, const swarm_adam_cfg* hp) {
   if (!c || !hp || c->n_agents < 1 || c->n_agents > 32 || c->n_envs < 1 || hp->batch < 1) return SWARM_E_BADARG;
   if (c->graph == SWARM_GRAPH_DENSE) return SWARM_E_BADARG;
   if (c->graph < 0 || c->graph > 3) return SWARM_E_BADARG;
+  if (c->net != SWARM_NET_GCN) return SWARM_E_UNSUPPORTED;   // GAT3: forward only
   if (c->graph == SWARM_GRAPH_KNN && (c->knn_k < 1 || c->knn_k > c->n_agents)) return SWARM_E_KNN_K;
   if (c->graph == SWARM_GRAPH_RADIUS && !(c->radius > 0.0f)) return SWARM_E_BADARG;
   if (hp->world_size < 1 || hp->update_target_every < 1) return SWARM_E_BADARG;

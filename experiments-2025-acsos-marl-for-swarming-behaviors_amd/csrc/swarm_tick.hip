@@ -53,7 +53,7 @@ size_t rec_bytes(int B, int N) { return (size_t)B * ho_stride_granules(N) * 8; }
 extern "C" {
 
 int swarm_train_tick_supported(const swarm_config* cfg) {
-  if (!cfg || cfg->n_agents < 1 || cfg->n_agents > 16 || cfg->n_envs < 1) return 0;
+  if (!cfg || cfg->n_agents < 1 || cfg->n_agents > 16 || cfg->n_envs < 1 || cfg->net != SWARM_NET_GCN) return 0;
   if (cfg->graph == SWARM_GRAPH_KNN && (cfg->knn_k < 1 || cfg->knn_k > cfg->n_agents)) return 0;
   if (cfg->graph == SWARM_GRAPH_RADIUS && !(cfg->radius > 0.0f)) return 0;
   return (cfg->graph == SWARM_GRAPH_COMPLETE || cfg->graph == SWARM_GRAPH_KNN || cfg->graph == SWARM_GRAPH_RADIUS) &&

@@ -43,6 +43,7 @@ SCENARIOS = {"GoTo": _lib.SWARM_GOTO, "ObstacleAvoidance": _lib.SWARM_OBSTACLE_A
              "obstacle_avoidance": _lib.SWARM_OBSTACLE_AVOIDANCE, "flocking": _lib.SWARM_FLOCKING}
 GRAPHS = {"complete": _lib.GRAPH_COMPLETE, "knn": _lib.GRAPH_KNN, "radius": _lib.GRAPH_RADIUS}
 CONVS = {"gat": _lib.CONV_GAT, "gcn": _lib.CONV_GCN}
+NETS = {"gcn": _lib.NET_GCN, "gat3": _lib.NET_GAT3}
 
 PARAM_ORDER = (
     ("conv1.att_src", (1, 1, 32)), ("conv1.att_dst", (1, 1, 32)), ("conv1.bias", (32,)),
@@ -50,14 +51,25 @@ PARAM_ORDER = (
     ("lin2.weight", (9, 32)), ("lin2.bias", (9,)),
 )
 
+# the three-layer GAT of the Flocking checkpoints (data/models/experiment_Flocking-seed_*.pth;
+# the GCN class with its commented conv2/conv3, train_gcn_dqn.py:54-55,65-68), hidden 8
+PARAM_ORDER_GAT3 = tuple(
+    (f"conv{i}.{n}", s) for i, k in ((1, 7), (2, 8), (3, 8))
+    for n, s in (("att_src", (1, 1, 8)), ("att_dst", (1, 1, 8)), ("bias", (8,)), ("lin.weight", (8, k))))
+PARAM_ORDER_GAT3 += (("lin1.weight", (8, 8)), ("lin1.bias", (8,)), ("lin2.weight", (9, 8)), ("lin2.bias", (9,)))
 
-def flatten_state_dict(sd, device=None) -> torch.Tensor:
-    return torch.cat([sd[k].detach().reshape(-1).to(torch.float32) for k, _ in PARAM_ORDER]).to(device)
+
+def param_order(net: str = "gcn"):
+    return PARAM_ORDER_GAT3 if net == "gat3" else PARAM_ORDER
 
 
-def unflatten_params(flat: torch.Tensor) -> dict:
+def flatten_state_dict(sd, device=None, net: str = "gcn") -> torch.Tensor:
+    return torch.cat([sd[k].detach().reshape(-1).to(torch.float32) for k, _ in param_order(net)]).to(device)
+
+
+def unflatten_params(flat: torch.Tensor, net: str = "gcn") -> dict:
     out, o = {}, 0
-    for k, shape in PARAM_ORDER:
+    for k, shape in param_order(net):
         n = math.prod(shape)
         out[k] = flat[o:o + n].reshape(shape).clone()
         o += n
@@ -96,15 +108,18 @@ class SwarmEngine:
                  adam_eps: float = 1e-8, max_norm: float = 1.0, update_target_every: int = 200,
                  replay_capacity: int = 1_000_000, env_offset: int = 0, world_size: int = 1,
                  process_group=None, shared_reset: bool = False, random_oa: bool = True, eps: float = 0.05,
-                 device=None, learn: bool = True):
+                 device=None, learn: bool = True, net: str = "gcn"):
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.type != "cuda":
             raise RuntimeError("SwarmEngine runs on a ROCm GPU only (no CPU fallback)")
         sid = SCENARIOS[scenario] if isinstance(scenario, str) else int(scenario)
         flags = (_lib.F_SHARED_RESET if shared_reset else 0) | (_lib.F_RANDOM_OA if random_oa else 0)
+        if net == "gat3" and learn:
+            raise ValueError("net='gat3' (the Flocking checkpoints' three-layer GAT) is forward only: use learn=False")
+        self.net = net
         self.cfg = SwarmConfig(n_envs, n_agents, sid, GRAPHS[graph], knn_k, CONVS[conv], env_offset, flags,
-                               seed & 0xFFFFFFFFFFFFFFFF, float(radius), 0)
+                               seed & 0xFFFFFFFFFFFFFFFF, float(radius), NETS[net])
         self.B, self.N = n_envs, n_agents
         self.scenario_id = sid
         self.batch = n_envs if batch is None else batch
@@ -115,19 +130,22 @@ class SwarmEngine:
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         self.state = torch.zeros(n_envs, n_agents, 4, **f32)
+        n_par = _lib.GAT3_N_PARAMS if net == "gat3" else N_PARAMS
         if params is None:
+            if net == "gat3":
+                raise ValueError("net='gat3' needs params (a Flocking checkpoint)")
             g = torch.Generator().manual_seed(seed)
             params = glorot_init(g)
         elif isinstance(params, dict):
-            params = flatten_state_dict(params)
+            params = flatten_state_dict(params, net=net)
         p0 = params.detach().to(**f32).reshape(-1)
-        assert p0.numel() == N_PARAMS
+        assert p0.numel() == n_par
         # learner buffers: [w_cur, w_nxt, m_cur, m_nxt, v_cur, v_nxt, target] rows + grad
         self._lrn = torch.zeros(7, N_PARAMS + 3, **f32)       # +3: rows stay 16-B aligned
-        self.params, self.w_nxt = self._lrn[0, :N_PARAMS], self._lrn[1, :N_PARAMS]
-        self.adam_m, self.m_nxt = self._lrn[2, :N_PARAMS], self._lrn[3, :N_PARAMS]
-        self.adam_v, self.v_nxt = self._lrn[4, :N_PARAMS], self._lrn[5, :N_PARAMS]
-        self.target = self._lrn[6, :N_PARAMS]
+        self.params, self.w_nxt = self._lrn[0, :n_par], self._lrn[1, :n_par]
+        self.adam_m, self.m_nxt = self._lrn[2, :n_par], self._lrn[3, :n_par]
+        self.adam_v, self.v_nxt = self._lrn[4, :n_par], self._lrn[5, :n_par]
+        self.target = self._lrn[6, :n_par]
         self.params.copy_(p0)
         self.target.copy_(p0)
         self.ctrl = torch.zeros(_lib.CTRL_WORDS, dtype=torch.int32, device=dev)
@@ -141,7 +159,7 @@ class SwarmEngine:
         self.rep_r = torch.zeros(cap, n_envs, n_agents, **f32)
         self.rep_a = torch.zeros(cap, n_envs, n_agents, dtype=torch.uint8, device=dev)
         self.replay = SwarmReplay(ptr(self.rep_s), ptr(self.rep_s1), ptr(self.rep_r), ptr(self.rep_a), cap, 0)
-        ws = self.lib.swarm_td_workspace_floats(ctypes_ref(self.cfg), self.batch)
+        ws = self.lib.swarm_td_workspace_floats(ctypes_ref(self.cfg), self.batch) if net == "gcn" else 4
         if ws < 0:
             check(int(ws), "swarm_td_workspace_floats")
         self.slabs = torch.zeros(int(ws), **f32)
@@ -328,11 +346,12 @@ class SwarmEngine:
 
     # ------------------------------------------------------------------ weights
     def state_dict(self) -> dict:
-        self.flush()
-        return unflatten_params(self.params.detach().cpu())
+        if self.net == "gcn":
+            self.flush()
+        return unflatten_params(self.params.detach().cpu(), self.net)
 
     def load_state_dict(self, sd):
-        self.params.copy_(flatten_state_dict(sd).to(self.device))
+        self.params.copy_(flatten_state_dict(sd, net=self.net).to(self.device))
         self.target.copy_(self.params)
 
 

@@ -10,6 +10,12 @@ lin1 -> relu -> lin2 for every graph of the batch in one HIP launch
 learner's backward is the fused hand-written one in ``swarm_td_grad``.
 ``conv="gcn"`` selects the GCNConv variant (parity unpinned), which
 reuses conv1.lin.weight / conv1.bias and ignores the attention vectors.
+
+``GCN(7, 8, 9, layers=3)`` is the same class with its commented conv2/conv3 layers
+(train_gcn_dqn.py:54-55, 65-68): conv1 -> tanh -> conv2 -> relu -> conv3 -> relu ->
+lin1 -> relu -> lin2, hidden 8 — the architecture of the reference's Flocking checkpoints
+(``data/models/experiment_Flocking-seed_*.pth``), forward only (``SWARM_NET_GAT3``).
+``GCN.from_state_dict(sd)`` picks the architecture from the checkpoint's keys.
 """
 from __future__ import annotations
 
@@ -18,7 +24,7 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import check, ptr, stream_ptr
-from .engine import PARAM_ORDER
+from .engine import param_order
 from .graph import Data, _lib_byref, _round4, edges_to_mult
 
 
@@ -39,22 +45,41 @@ class GATConvParams(nn.Module):
 
 
 class GCN(nn.Module):
-    def __init__(self, input_dim: int = 7, hidden_dim: int = 32, output_dim: int = 9, conv: str = "gat"):
+    def __init__(self, input_dim: int = 7, hidden_dim: int = 32, output_dim: int = 9, conv: str = "gat",
+                 layers: int = 1):
         super().__init__()
-        if (input_dim, hidden_dim, output_dim) != (7, 32, 9):
-            raise ValueError("the HIP kernels are specialised for GCN(7, 32, 9) (train_gcn_dqn.py:81)")
+        shapes = {1: (7, 32, 9), 3: (7, 8, 9)}
+        if shapes.get(layers) != (input_dim, hidden_dim, output_dim):
+            raise ValueError("the HIP kernels are specialised for GCN(7, 32, 9) (train_gcn_dqn.py:81) and the "
+                             "Flocking checkpoints' GCN(7, 8, 9, layers=3)")
+        if layers == 3 and conv != "gat":
+            raise ValueError("the three-layer network is a GAT")
         self.conv1 = GATConvParams(input_dim, hidden_dim)
+        if layers == 3:
+            self.conv2 = GATConvParams(hidden_dim, hidden_dim)
+            self.conv3 = GATConvParams(hidden_dim, hidden_dim)
         self.lin1 = nn.Linear(hidden_dim, hidden_dim)
         self.lin2 = nn.Linear(hidden_dim, output_dim)
         self.conv = conv
+        self.layers = layers
+        self.net = "gat3" if layers == 3 else "gcn"
+        self.net_id = _lib.NET_GAT3 if layers == 3 else _lib.NET_GCN
         self._flat = None
         self._flat_key = None
 
+    @classmethod
+    def from_state_dict(cls, sd, conv: str = "gat") -> "GCN":
+        """A model of the checkpoint's architecture (three GATConvs if it holds conv2), loaded."""
+        m = cls(7, 8, 9, conv, layers=3) if "conv2.lin.weight" in sd else cls(7, 32, 9, conv)
+        m.load_state_dict(sd)
+        return m
+
     def flat_params(self, device="cuda") -> torch.Tensor:
         sd = dict(self.named_parameters())
-        key = tuple((id(sd[k]), sd[k]._version) for k, _ in PARAM_ORDER) + (str(device),)
+        order = param_order(self.net)
+        key = tuple((id(sd[k]), sd[k]._version) for k, _ in order) + (str(device),)
         if self._flat is None or self._flat_key != key:
-            self._flat = torch.cat([sd[k].detach().reshape(-1) for k, _ in PARAM_ORDER]).to(device, torch.float32)
+            self._flat = torch.cat([sd[k].detach().reshape(-1) for k, _ in order]).to(device, torch.float32)
             self._flat_key = key
         return self._flat
 
@@ -68,7 +93,7 @@ class GCN(nn.Module):
         if data.swarm is not None:
             m = data.swarm
             cfg = _lib.SwarmConfig(m["n_graphs"], m["n_nodes"], 0, m["graph"], m["k"], conv, 0, 0, 0,
-                                   float(m.get("radius", 0.0)), 0)
+                                   float(m.get("radius", 0.0)), self.net_id)
             check(lib.swarm_q_forward(_lib_byref(cfg), ptr(params), ptr(x), None, ptr(q), stream_ptr()),
                   "swarm_q_forward")
         else:
@@ -77,7 +102,7 @@ class GCN(nn.Module):
                 raise ValueError("GCN.forward: graphs of unequal size are not supported")
             N = M // G
             mult = edges_to_mult(data.edge_index, G, N)
-            cfg = _lib.SwarmConfig(G, N, 0, _lib.GRAPH_DENSE, 0, conv, 0, 0, 0)
+            cfg = _lib.SwarmConfig(G, N, 0, _lib.GRAPH_DENSE, 0, conv, 0, 0, 0, 0.0, self.net_id)
             check(lib.swarm_q_forward(_lib_byref(cfg), ptr(params), ptr(x), ptr(mult), ptr(q), stream_ptr()),
                   "swarm_q_forward")
         return q

@@ -52,8 +52,9 @@ class Simulator:
         eng = self.env.engine
         params = self.model.flat_params(eng.device)
         conv = _lib.CONV_GAT if getattr(self.model, "conv", "gat") == "gat" else _lib.CONV_GCN
-        saved = (eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius)
+        saved = (eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius, eng.cfg.net)
         eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius = self.graph, self.knn_k, conv, self.radius
+        eng.cfg.net = getattr(self.model, "net_id", _lib.NET_GCN)   # the Flocking checkpoints' GAT3
         T = self.env.max_steps
         try:
             for episode in range(self.episodes):
@@ -75,7 +76,7 @@ class Simulator:
                 self.distance_at_the_beginning.append(dist[0])
                 self.episode_rewards.append(float(total_reward) / T)
         finally:
-            eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius = saved
+            eng.cfg.graph, eng.cfg.knn_k, eng.cfg.conv, eng.cfg.radius, eng.cfg.net = saved
         self.save_metrics_to_csv()
 
     def save_metrics_to_csv(self):

@@ -34,6 +34,13 @@ extern "C" {
 enum swarm_scenario { SWARM_GOTO = 0, SWARM_OBSTACLE_AVOIDANCE = 1, SWARM_FLOCKING = 2 };
 enum swarm_graph { SWARM_GRAPH_COMPLETE = 0, SWARM_GRAPH_KNN = 1, SWARM_GRAPH_DENSE = 2, SWARM_GRAPH_RADIUS = 3 };
 enum swarm_conv { SWARM_CONV_GAT = 0, SWARM_CONV_GCN = 1 };
+/* Q-network: GCN = the reference's GCN class (one GATConv, hidden 32; params N_PARAMS = 1673;
+   trainable).  GAT3 = the same class with its commented conv2/conv3 layers (train_gcn_dqn.py:54-55,
+   65-68), hidden 8, 409 params: what data/models/experiment_Flocking-seed_*.pth hold.  GAT3 is
+   forward only (swarm_q_forward, swarm_act_step, swarm_rollout); the learner entry points return
+   SWARM_E_UNSUPPORTED for it. */
+enum swarm_net { SWARM_NET_GCN = 0, SWARM_NET_GAT3 = 1 };
+#define SWARM_GAT3_N_PARAMS 409
 
 /* Static description of a batch of vectorised environments (one rank's shard). */
 typedef struct swarm_config {
@@ -50,7 +57,7 @@ typedef struct swarm_config {
   int32_t flags;        /* SWARM_F_* bits                                               */
   uint64_t seed;        /* Philox key                                                   */
   float radius;         /* neighbour radius of SWARM_GRAPH_RADIUS (> 0)                 */
-  int32_t pad;
+  int32_t net;          /* swarm_net (GAT3 requires conv == SWARM_CONV_GAT)             */
 } swarm_config;
 
 #define SWARM_F_SHARED_RESET 1   /* one reset centre for all envs (go_to_position_scenario.py:88) */

@@ -452,6 +452,64 @@ def q_forward_dense(params: dict, x: torch.Tensor, mult: torch.Tensor, return_al
     return q
 
 
+def gat_conv_dense(x: torch.Tensor, mult: torch.Tensor, W, att_src, att_dst, bias) -> torch.Tensor:
+    """One GATConv of q_forward_dense for [B,N] graphs (any width)."""
+    h = F.linear(x, W)
+    a_s = (h * att_src.reshape(1, 1, -1)).sum(-1)
+    a_d = (h * att_dst.reshape(1, 1, -1)).sum(-1)
+    e = F.leaky_relu(a_s[:, :, None] + a_d[:, None, :], 0.2)
+    present = mult > 0
+    emax = torch.where(present, e.detach(), torch.tensor(float("-inf"))).amax(dim=1)
+    emax = torch.where(torch.isinf(emax), torch.zeros_like(emax), emax)
+    ex = torch.where(present, (e - emax[:, None, :]).exp(), torch.zeros_like(e))
+    den = (mult * ex).sum(dim=1) + 1e-16
+    return torch.einsum("buv,buh->bvh", mult * (ex / den[:, None, :]), h) + bias
+
+
+GAT3_PARAM_ORDER = tuple(
+    (f"conv{i}.{n}", s) for i, k in ((1, 7), (2, 8), (3, 8))
+    for n, s in (("att_src", (1, 1, 8)), ("att_dst", (1, 1, 8)), ("bias", (8,)), ("lin.weight", (8, k))))
+GAT3_PARAM_ORDER += (("lin1.weight", (8, 8)), ("lin1.bias", (8,)), ("lin2.weight", (9, 8)), ("lin2.bias", (9,)))
+GAT3_N_PARAMS = sum(int(np.prod(s)) for _, s in GAT3_PARAM_ORDER)   # 409
+
+
+def gat3_unflatten(flat) -> dict:
+    flat = torch.as_tensor(flat, dtype=torch.float32)
+    out, o = {}, 0
+    for k, shape in GAT3_PARAM_ORDER:
+        n = int(np.prod(shape))
+        out[k] = flat[o:o + n].reshape(shape).clone()
+        o += n
+    return out
+
+
+def gat3_q_forward_edges(params: dict, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+    """The Flocking checkpoints' network (data/models/experiment_Flocking-seed_*.pth): GCN.forward
+    with its commented layers (train_gcn_dqn.py:54-55, 62-70): conv1 -> tanh -> conv2 -> relu
+    -> conv3 -> relu -> lin1 -> relu -> lin2, hidden 8.  Parity unpinned (no recorded Flocking
+    outputs); the checkpoints' shapes are the architecture's only pin."""
+    def conv(i, z):
+        return gat_conv_edges(z, edge_index, params[f"conv{i}.lin.weight"], params[f"conv{i}.att_src"],
+                              params[f"conv{i}.att_dst"], params[f"conv{i}.bias"])
+    z = torch.tanh(conv(1, x))
+    z = torch.relu(conv(2, z))
+    z = torch.relu(conv(3, z))
+    z = torch.relu(F.linear(z, params["lin1.weight"], params["lin1.bias"]))
+    return F.linear(z, params["lin2.weight"], params["lin2.bias"])
+
+
+def gat3_q_forward_dense(params: dict, x: torch.Tensor, mult: torch.Tensor) -> torch.Tensor:
+    """gat3_q_forward_edges for [B,N] graphs given by a dense multiplicity."""
+    def conv(i, z):
+        return gat_conv_dense(z, mult, params[f"conv{i}.lin.weight"], params[f"conv{i}.att_src"],
+                              params[f"conv{i}.att_dst"], params[f"conv{i}.bias"])
+    z = torch.tanh(conv(1, x))
+    z = torch.relu(conv(2, z))
+    z = torch.relu(conv(3, z))
+    z = torch.relu(F.linear(z, params["lin1.weight"], params["lin1.bias"]))
+    return F.linear(z, params["lin2.weight"], params["lin2.bias"])
+
+
 def gcn_conv_dense(params: dict, x: torch.Tensor, mult: torch.Tensor):
     """a13 (PARITY UNPINNED, not in the reference): PyG 2.5.3 GCNConv defaults on the
     same multigraph: add_remaining_self_loops (self loops collapse to one weight-1
@@ -537,7 +595,9 @@ def act_tick(params: dict, pos, vel, scenario: int, graph: int, k: int, eps: flo
     B, N, _ = pos.shape
     x = node_features(pos, vel)
     mult = graph_multiplicity(pos, graph, k, radius)
-    if conv == "gat":
+    if "conv2.lin.weight" in params:   # the three-layer GAT (Flocking checkpoints)
+        q = gat3_q_forward_dense(params, x, mult)
+    elif conv == "gat":
         q = q_forward_dense(params, x, mult)
     else:
         q = gcn_conv_dense(params, x, mult)

@@ -18,7 +18,9 @@ def pytest_configure(config):
 def golden_weights():
     import numpy as np
     z = np.load(os.path.join(GOLDEN, "weights.npz"))
-    return {"go_to": z["weights_go_to"], "obstacle_avoidance": z["weights_obstacle_avoidance"]}
+    f = np.load(os.path.join(GOLDEN, "flocking_weights.npz"))
+    return {"go_to": z["weights_go_to"], "obstacle_avoidance": z["weights_obstacle_avoidance"],
+            "flocking_gat3": f["weights_flocking"]}
 
 
 @pytest.fixture(scope="session")

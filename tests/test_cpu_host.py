@@ -121,6 +121,13 @@ def test_fused_tick_support_and_workspace_host_side():
     args = (ctypes.byref(hp), ctypes.byref(lr), 1, ctypes.byref(rp), 1, None, 1, 1, None, None)
     assert lib.swarm_train_tick(ctypes.byref(bad[0]), *args) == -4
     assert lib.swarm_train_tick(ctypes.byref(ok[0]), *args[:6], 1, None, None, None) == -1   # no workspace
+    # the three-layer GAT (Flocking checkpoints) is forward only: every learner entry point refuses it
+    g3 = L.SwarmConfig(64, 8, 2, 0, 5, 0, 0, 0, 0, 0.0, L.NET_GAT3)
+    assert lib.swarm_train_tick_supported(ctypes.byref(g3)) == 0
+    assert lib.swarm_td_grad(ctypes.byref(g3), ctypes.byref(hp), 1, 1, ctypes.byref(rp), 1, None, None, 1,
+                             None) == -4
+    assert lib.swarm_train_act_step(ctypes.byref(g3), ctypes.byref(hp), ctypes.byref(lr), 1, ctypes.byref(rp), 1,
+                                    None, None, None) == -4
 
 
 @pytest.mark.parametrize("n", [1, 5, 8, 12])

@@ -84,3 +84,29 @@ def test_reset_centre_distribution():
     mean = c.double().mean(0)
     assert math.isclose(mean[0].item(), -1.6, abs_tol=0.03) and math.isclose(mean[1].item(), 1.6, abs_tol=0.03)
     assert math.isclose(c.double().std(0)[0].item(), 0.4, abs_tol=0.03)
+
+
+# ---------------------------------------------------------------- the Flocking checkpoints' GAT3
+def test_gat3_dense_equals_edge_list(golden_weights):
+    for seed, N, graph in ((0, 2, O.GRAPH_COMPLETE), (3, 5, O.GRAPH_KNN), (7, 8, O.GRAPH_COMPLETE),
+                           (9, 12, O.GRAPH_KNN)):
+        P = O.gat3_unflatten(golden_weights["flocking_gat3"][seed])
+        g = torch.Generator().manual_seed(seed)
+        pos, vel = torch.randn(6, N, 2, generator=g) * 0.4, torch.randn(6, N, 2, generator=g) * 0.2
+        x = O.node_features(pos, vel)
+        mult = O.graph_multiplicity(pos, graph, k=min(5, N))
+        q_dense = O.gat3_q_forward_dense(P, x, mult)
+        q_edges = O.gat3_q_forward_edges(P, x.reshape(-1, 7), O.edge_index_from_multiplicity(mult))
+        assert torch.allclose(q_dense.reshape(-1, 9), q_edges, rtol=1e-5, atol=1e-5)
+
+
+def test_gat3_host_layout_matches_the_checkpoints(golden_weights):
+    import swarm_amd
+    from swarm_amd.engine import PARAM_ORDER_GAT3, flatten_state_dict, unflatten_params
+    assert PARAM_ORDER_GAT3 == O.GAT3_PARAM_ORDER and O.GAT3_N_PARAMS == 409
+    flat = torch.tensor(golden_weights["flocking_gat3"][4])
+    sd = unflatten_params(flat, "gat3")
+    m = swarm_amd.GCN.from_state_dict(sd)
+    assert m.layers == 3 and m.net == "gat3"
+    assert torch.equal(m.flat_params("cpu"), flat) and torch.equal(flatten_state_dict(sd, net="gat3"), flat)
+    assert list(m.state_dict()) == [k for k, _ in O.GAT3_PARAM_ORDER]   # the .pth key order

@@ -523,6 +523,93 @@ def test_graph_capture_replay_equals_eager(sw, golden_weights):
     assert a.read_ctrl() == b.read_ctrl()
 
 
+# ------------------------------------------------------------------ the Flocking checkpoints' GAT3 (forward only)
+def _gat3(golden_weights, seed):
+    flat = torch.tensor(golden_weights["flocking_gat3"][seed])
+    return flat, O.gat3_unflatten(flat)
+
+
+@pytest.mark.parametrize("N", [2, 5, 8, 12, 20, 32])
+@pytest.mark.parametrize("graph", ["complete", "knn", "radius"])
+def test_gat3_q_forward_parity(sw, golden_weights, N, graph):
+    """GCN(7, 8, 9, layers=3) loaded from experiment_Flocking-seed_*.pth (fixture) vs the oracle.
+    Parity unpinned beyond the oracle: the reference records no Flocking outputs."""
+    B = 64
+    flat, P = _gat3(golden_weights, N % 10)
+    model = sw.GCN.from_state_dict(P)
+    pos, vel = _rand_state(B, N, 40 + N, tight=(N == 12))
+    obs = torch.cat([pos, vel, O.f32(O.GOAL).expand(B, N, 2)], -1)
+    k = min(5, N)
+    if graph == "complete":
+        data, mult = sw.create_graph_from_observations(obs), O.multiplicity_complete(B, N)
+    elif graph == "knn":
+        data, mult = sw.create_knn_graph_from_observations(obs, N, k), O.multiplicity_knn(O.knn_sets(pos, k))
+    else:
+        data = sw.create_radius_graph_from_observations(obs, N, 0.3)
+        mult = O.multiplicity_radius(O.radius_sets(pos, 0.3))
+    q = model(data).cpu().view(B, N, 9)
+    ref = O.gat3_q_forward_dense(P, O.node_features(pos, vel), mult)
+    assert_close_rel(q, ref, 1e-5, "Q(gat3)")
+    m = _tie_mask(ref)
+    assert torch.equal(q.argmax(-1)[m], ref.argmax(-1)[m])
+
+
+def test_gat3_q_forward_from_pyg_edge_index(sw, golden_weights):
+    N, G = 6, 7
+    flat, P = _gat3(golden_weights, 3)
+    model = sw.GCN.from_state_dict(P)
+    pos, vel = _rand_state(G, N, 8)
+    datas = [sw.Data(x=O.node_features(pos[g:g + 1], vel[g:g + 1])[0], edge_index=O.knn_edge_index(pos[g], 3))
+             for g in range(G)]
+    batch = sw.Batch.from_data_list(datas)
+    q = model(batch).cpu()
+    assert_close_rel(q, O.gat3_q_forward_edges(P, batch.x, batch.edge_index), 1e-5, "Q(gat3, edge_index)")
+
+
+@pytest.mark.parametrize("N,graph", [(8, "knn"), (5, "complete"), (12, "radius")])
+def test_gat3_flocking_rollout_matches_oracle_ticks(sw, golden_weights, N, graph):
+    """The Flocking checkpoints acting in the Flocking scenario: one swarm_rollout launch vs the
+    oracle's graph -> GAT3 -> argmax -> env.step -> shaped reward, tick by tick (greedy)."""
+    B, T = 48, 6
+    flat, P = _gat3(golden_weights, 1)
+    eng = sw.SwarmEngine("Flocking", N, B, seed=2, params=flat, graph=graph, knn_k=5, radius=0.3, learn=False,
+                         net="gat3", eps=0.0)
+    eng.reset(0)
+    torch.cuda.synchronize()
+    st = eng.state.cpu()
+    pos, vel = st[..., :2].clone(), st[..., 2:].clone()
+    r = eng.rollout(T, tick0=0, eps=0.0, traj=True)
+    torch.cuda.synchronize()
+    gid = {"complete": O.GRAPH_COMPLETE, "knn": O.GRAPH_KNN, "radius": O.GRAPH_RADIUS}[graph]
+    rew = torch.zeros(B, N)
+    ok = torch.ones(B, dtype=torch.bool)   # envs whose greedy actions were clear of Q near-ties so far
+    for t in range(T):
+        ref = O.act_tick(P, pos, vel, O.SCENARIO_FLOCK, gid, 5, 0.0, 2, t, radius=0.3)
+        ok &= _tie_mask(ref.q).all(-1)
+        got = r["traj_pos"][t].cpu()
+        assert (got[ok] - ref.step["pos"][ok]).abs().max() <= 1e-5, t
+        pos, vel = ref.step["pos"], ref.step["vel"]
+        rew += ref.step["rew"]
+    assert ok.float().mean() > 0.8
+    err = (r["reward"].cpu()[ok] - rew[ok]).abs().max()
+    assert err <= 1e-3, err   # T summed flocking rewards (x10-shaped differences)
+
+
+def test_gat3_simulator_drop_in(sw, golden_weights, tmp_path):
+    """Simulator(env, model, ...) with a Flocking checkpoint in the Flocking scenario."""
+    flat, P = _gat3(golden_weights, 0)
+    model = sw.GCN.from_state_dict(P)
+    env = sw.make_env(sw.get_scenario("Flocking"), num_envs=1, continuous_actions=False, max_steps=15,
+                      dict_spaces=True, seed=3, n_agents=6)
+    sim = sw.Simulator(env, model, 2, "flocking", 3, output_dir=str(tmp_path / "sim"), knn_k=5)
+    sim.run_simulation()
+    import csv
+    assert len(list(csv.reader(open(tmp_path / "sim" / "result.csv")))) == 3
+    assert env.engine.cfg.net == 0   # the env's own network setting restored
+    with pytest.raises(ValueError):
+        sw.SwarmEngine("Flocking", 6, 4, params=flat, net="gat3", learn=True)
+
+
 # ------------------------------------------------------------------ reference API drop-in
 def test_make_env_api_drop_in(sw):
     env = sw.make_env(sw.GoToPositionScenario(), num_envs=1, device="cpu", continuous_actions=False, wrapper=None,
