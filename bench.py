@@ -55,6 +55,13 @@ def gcn_fwd_flops(N: int, d: float) -> float:
     return 448 + 67 * d + 64 + 2080 + 32 + 585
 
 
+def gat3_fwd_flops(N: int, d: float) -> float:
+    """The Flocking checkpoints' three-layer GAT (hidden 8) per node: lins 7->8 (112) and 8->8
+    (2 x 128), scores (3 x 32), softmax + aggregate per edge (3 x (5 + 16)), bias + activation
+    (3 x 16), lin1 (128 + 8), relu (8), lin2 (144 + 9)."""
+    return 112 + 256 + 96 + 63 * d + 48 + 136 + 8 + 153
+
+
 def gcn_bwd_flops(N: int, d: float) -> float:
     return 32 + 32 + 2048 + 96 + 64 * d + 2048 + 64 + 448 + 32 * 2 + 9
 
@@ -97,6 +104,8 @@ def parse():
     ap.add_argument("--tick", default="fused", choices=("fused", "3"),
                     help="fused: acting + TD blocks in one launch (swarm_train_tick) where supported; "
                          "3: act / TD / reduce launches")
+    ap.add_argument("--net", default="gcn", choices=("gcn", "gat3"),
+                    help="gat3: the Flocking checkpoints' three-layer GAT (acting only, --mode act)")
     ap.add_argument("--batch", type=int, default=None, help="sampled graphs per update per GPU (default = envs)")
     ap.add_argument("--chunk", type=int, default=20, help="ticks per captured hipGraph")
     ap.add_argument("--no-graph", action="store_true")
@@ -132,12 +141,18 @@ def main():
     shard = swdist.Shard(rank, world, B)
     S = args.batch or B
     scen = args.scenario
-    wkey = "weights_go_to" if scen == "GoTo" else "weights_obstacle_avoidance"
-    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
+    if args.net == "gat3":
+        if args.mode != "act":
+            raise SystemExit("--net gat3 is forward only: use --mode act")
+        w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "flocking_weights.npz"))["weights_flocking"][0])
+    else:   # Flocking trains the one-layer network: start it from GoTo's checkpoint
+        wkey = "weights_obstacle_avoidance" if scen == "ObstacleAvoidance" else "weights_go_to"
+        w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
     eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=shard.env_offset,
                                 world_size=world, process_group=pg, update_target_every=200,
-                                replay_capacity=1_000_000, conv=args.conv, graph=args.graph, knn_k=args.knn_k,
-                                radius=args.radius)
+                                replay_capacity=1_000_000 if args.net == "gcn" else 1, conv=args.conv,
+                                graph=args.graph, knn_k=args.knn_k, radius=args.radius, net=args.net,
+                                learn=args.net == "gcn")
     max_steps = 100
     if args.mode == "act":
         return bench_act(args, eng, world, rank, distributed, max_steps)
@@ -284,7 +299,8 @@ def main():
         pmc = os.path.join(ROOT, "profiles", pmcf)
         if os.path.exists(pmc) and headline:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        roof = {"bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        roof = {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
+                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": kname,
                 "algorithmic_flops_per_launch": flops,
                 "algorithmic_bytes_per_launch": nbytes,
@@ -360,7 +376,10 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     d = mean_in_degree(args, eng)
-    f_node = (gat_fwd_flops(N, d) if args.conv == "gat" else gcn_fwd_flops(N, d)) + 300   # + physics
+    if args.net == "gat3":
+        f_node = gat3_fwd_flops(N, d) + 300
+    else:
+        f_node = (gat_fwd_flops(N, d) if args.conv == "gat" else gcn_fwd_flops(N, d)) + 300   # + physics
     roof = None
     if not args.no_kernel_timing:   # one 100-tick rollout launch, HIP events on its stream
         stream = torch.cuda.current_stream()
@@ -376,7 +395,8 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
         t_l = float(np.median(per))
         flops = B * N * max_steps * f_node
         ach = flops / t_l / 1e12
-        roof = {"bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        roof = {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
+                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP32_TFLOPS, "traffic": None, "kernel": "act_kernel rollout (swarm_rollout)",
                 "algorithmic_flops_per_launch": flops, "launch_us": round(t_l * 1e6, 2)}
     if rank == 0:
@@ -385,7 +405,8 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
                 "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference seed_0 weights)",
-                "config": {"workload": f"{args.scenario} acting-only: {N} agents x {B} envs/GPU, {args.conv.upper()}, "
+                "config": {"workload": f"{args.scenario} acting-only: {N} agents x {B} envs/GPU, "
+                                       f"{'GAT3 (Flocking checkpoints)' if args.net == 'gat3' else args.conv.upper()}, "
                                        f"{g} graph, eps 0, frozen weights", "envs_per_gpu": B, "agents": N,
                            "global_envs": B * world, "graph": args.graph, "conv": args.conv,
                            "parallelism": f"replicas x{world}"},

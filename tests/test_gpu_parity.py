@@ -653,6 +653,21 @@ def test_simulator_and_trainer_smoke(sw, golden_weights, tmp_path):
     assert rows[0] == ["Episode", "Reward", "Loss"] and rows[1][0] == "9"
 
 
+def test_flocking_trainer_drop_in(sw, tmp_path):
+    """train_gcn_dqn.py's train_model('Flocking'): the reference's one-layer GCN trained in the
+    Flocking scenario (get_scenario :244-245), checkpoint and stats written in its layout."""
+    import csv
+    env = sw.make_env(sw.get_scenario("Flocking"), num_envs=4, continuous_actions=False, max_steps=10,
+                      dict_spaces=True, seed=0, n_agents=6)
+    tr = sw.DQNTrainer(env, 0, str(tmp_path / "models"), str(tmp_path / "stats"), "Flocking", batch_size=8)
+    tr.train_model({"epsilon": 0.99, "epsilon_decay": 0.01, "min_epsilon": 0.05, "episodes": 10})
+    sd = torch.load(tmp_path / "models" / "experiment_Flocking-seed_0.pth", weights_only=True)
+    assert list(sd.keys()) == [k for k, _ in O.PARAM_ORDER] and all(torch.isfinite(v).all() for v in sd.values())
+    rows = list(csv.reader(open(tmp_path / "stats" / "experiment_Flocking-seed_0.csv")))   # a row per 10 episodes
+    assert rows[0] == ["Episode", "Reward", "Loss"] and rows[-1][0] == "9"
+    assert all(float(r[2]) >= 0.0 for r in rows[1:])
+
+
 def test_training_curve_matches_reference_statistically(sw):
     """Training-path parity (unpinned bit for bit): DQNTrainer.train_model
     with the reference script's configuration (train_gcn_dqn.py:262-290; 10 agents, 1 env,

@@ -27,6 +27,12 @@ RUNS += [
     # the north_star's radius-neighbour graph (not in the reference; 3-launch tick for training)
     ("C2 GoTo 8x1024 GAT act radius-0.3", ["--mode", "act", "--graph", "radius", "--radius", "0.3"]),
     ("C2 GoTo 8x1024 GAT train radius-0.3", ["--graph", "radius", "--radius", "0.3"]),
+    # the Flocking scenario (one-layer GCN training, as train_model('Flocking'))
+    # and the Flocking checkpoints' three-layer GAT acting
+    ("Flocking 8x1024 GAT train", ["--scenario", "Flocking"]),
+    ("Flocking 8x1024 GAT3 act kNN-5", ["--scenario", "Flocking", "--mode", "act", "--net", "gat3",
+                                        "--graph", "knn", "--knn-k", "5"]),
+    ("Flocking 8x1024 GAT3 act complete", ["--scenario", "Flocking", "--mode", "act", "--net", "gat3"]),
 ]
 
 if len(sys.argv) > 2:
