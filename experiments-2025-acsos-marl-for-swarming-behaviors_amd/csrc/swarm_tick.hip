@@ -118,13 +118,13 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
     else if (spec == SPEC_COMPLETE_GCN) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GCN); \
     else SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_RUNTIME);                                 \
   } while (0)
-  const bool fl = cfg->scenario == SWARM_FLOCKING;   // flocking: the runtime-switched kernel only
+  const bool fl = cfg->scenario == SWARM_FLOCKING;
   if (N <= 8) {
-    if (fl) SWARM_TICK_LAUNCH(8, 8, SWARM_FLOCKING, SPEC_RUNTIME);
+    if (fl) SWARM_TICK_LAUNCH2(8, 8, SWARM_FLOCKING);
     else if (oa) SWARM_TICK_LAUNCH2(8, 8, SWARM_OBSTACLE_AVOIDANCE);
     else SWARM_TICK_LAUNCH2(8, 8, SWARM_GOTO);
   } else {
-    if (fl) SWARM_TICK_LAUNCH(16, 16, SWARM_FLOCKING, SPEC_RUNTIME);
+    if (fl) SWARM_TICK_LAUNCH2(16, 16, SWARM_FLOCKING);
     else if (oa) SWARM_TICK_LAUNCH2(16, 16, SWARM_OBSTACLE_AVOIDANCE);
     else SWARM_TICK_LAUNCH2(16, 16, SWARM_GOTO);
   }
