@@ -20,6 +20,8 @@ for conv in ("gat", "gcn"):
                      ["--scenario", "ObstacleAvoidance", "--agents", str(n), "--envs", "512", "--conv", conv]))
 RUNS += [
     ("C2 GoTo 8x1024 GCN train", ["--conv", "gcn"]),
+    # also the reference's absolute TD batch, S = 32 graphs per tick
+    ("C2 GoTo 8x1024 GAT train S=32", ["--batch", "32"]),
     ("C2 GoTo 8x1024 GAT act kNN-5", ["--mode", "act", "--graph", "knn", "--knn-k", "5"]),
     ("C2 GoTo 8x1024 GAT act complete", ["--mode", "act"]),
     ("C3 OA 12x1024 GAT act kNN-10", ["--mode", "act", "--scenario", "ObstacleAvoidance", "--agents", "12",
