@@ -9,7 +9,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["swarm_act.hip", "swarm_td.hip", "swarm_tick.hip"]
-HEADERS = ["swarm_actk.h", "swarm_tdk.h", "swarm_common.h", "swarm_knn.h", "swarm_wpg.h", "swarm_dl.h", "swarm_env.h", "swarm_adam.h"]
+HEADERS = ["swarm_actk.h", "swarm_tdk.h", "swarm_common.h", "swarm_knn.h", "swarm_wpg.h", "swarm_dl.h", "swarm_env.h",
+           "swarm_adam.h", "swarm_gat3.h"]
 OUT = os.path.join(HERE, "libswarm_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # kernarg preload: the leading 14 kernel-argument dwords arrive in SGPRs at wave start (the
@@ -21,6 +22,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 
 def _deps():
     files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    files += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h") and f not in HEADERS]
     files.append(os.path.join(os.path.dirname(HERE), "include", "swarm_hip.h"))
     return files
 

@@ -25,6 +25,13 @@ constexpr int G3_N_PARAMS = 409;
 static_assert(g3_conv_off(2) + G3_W + kH3 * kH3 == G3_LIN1_W, "gat3 layout");
 static_assert(G3_N_PARAMS <= N_LDS_PARAMS, "gat3 weights fit the acting LDS image");
 
+// the first 8 floats of an LDS row (rows are 16-B aligned: kRow = 36)
+__device__ inline void load_row8(const float* row, float x[kH3]) {
+  const float4 a = *reinterpret_cast<const float4*>(row);
+  const float4 b = *reinterpret_cast<const float4*>(row + 4);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+}
+
 // Fills F.q (and sm.Q, sm.px / sm.py, the graph masks of sm) like dl_forward; P holds the
 // 409 weights unpadded.  F.x must hold the lane's features (zero for nodes >= N).
 template <int NS>
@@ -67,7 +74,14 @@ __device__ inline void gat3_forward(const float* __restrict__ P, const DGeom<NS>
     }
     wave_lds_sync();
   }
-#pragma unroll 1
+  // in-edge multiplicities of the lane's node: the same graph for all three layers
+  constexpr bool kKeepM = NS <= 16;   // registers: NS ints per column tile
+  int mk[kKeepM ? CT : 1][kKeepM ? NS : 1];
+  if constexpr (kKeepM) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) in_mults<NS>(min(16 * ct + c, NS - 1), N, graph, sm, dense, d.gid, mk[ct]);
+  }
+#pragma unroll
   for (int l = 0; l < 3; ++l) {
     const float* Pc = P + g3_conv_off(l);
     const int K = l == 0 ? kFeat : kH3;
@@ -77,8 +91,7 @@ __device__ inline void gat3_forward(const float* __restrict__ P, const DGeom<NS>
     for (int ct = 0; ct < CT; ++ct) {
       const int n = min(16 * ct + c, NS - 1);
       float x[kH3];
-#pragma unroll
-      for (int kk = 0; kk < kH3; ++kk) x[kk] = V.H[n][kk];
+      load_row8(&V.H[n][0], x);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const float* w = Pc + G3_W + (2 * p + i) * K;
@@ -104,7 +117,12 @@ __device__ inline void gat3_forward(const float* __restrict__ P, const DGeom<NS>
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c;
       int m[NS];
-      in_mults<NS>(min(n, NS - 1), N, graph, sm, dense, d.gid, m);
+      if constexpr (kKeepM) {
+#pragma unroll
+        for (int u = 0; u < NS; ++u) m[u] = mk[ct][u];
+      } else {
+        in_mults<NS>(min(n, NS - 1), N, graph, sm, dense, d.gid, m);
+      }
       float e[NS];
       float emax = -INFINITY;
 #pragma unroll
@@ -140,8 +158,7 @@ __device__ inline void gat3_forward(const float* __restrict__ P, const DGeom<NS>
   for (int ct = 0; ct < CT; ++ct) {
     const int n = min(16 * ct + c, NS - 1);
     float x[kH3];
-#pragma unroll
-    for (int kk = 0; kk < kH3; ++kk) x[kk] = V.H[n][kk];
+    load_row8(&V.H[n][0], x);
     float z[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -159,8 +176,7 @@ __device__ inline void gat3_forward(const float* __restrict__ P, const DGeom<NS>
   for (int ct = 0; ct < CT; ++ct) {
     const int n = min(16 * ct + c, NS - 1);
     float z[kH3];
-#pragma unroll
-    for (int kk = 0; kk < kH3; ++kk) z[kk] = V.R[n][kk];
+    load_row8(&V.R[n][0], z);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int a = p + 4 * j;
