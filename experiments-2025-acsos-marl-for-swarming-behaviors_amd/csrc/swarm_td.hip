@@ -44,14 +44,20 @@ struct ReduceArgs {
 // reproducible run to run.  Advance mode adds one control block (the last): it prepares
 // and stores the whole ctrl update (Adam scalars of the next step in double, the next
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
-constexpr int kRedCols = 16;
-constexpr int kRedGroups = 64;
+#ifndef SWARM_RED_COLS
+#define SWARM_RED_COLS 16
+#define SWARM_RED_GROUPS 64
+#endif
+constexpr int kRedCols = SWARM_RED_COLS;
+constexpr int kRedGroups = SWARM_RED_GROUPS;
+constexpr int kRedRuns = kRedGroups / 8;   // first combine level: runs of 8 group sums
+static_assert(kRedGroups % 8 == 0 && kRedCols * kRedGroups <= 1024, "reduce geometry");
 constexpr int kRedColBlocks = (N_PARAMS + 1 + kRedCols - 1) / kRedCols;
 // slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start
 __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(const float* slabs, swarm_ctrl* ctrl,
                                                                             int n_slabs, int advance, ReduceArgs A) {
   __shared__ float part[kRedGroups][kRedCols];
-  __shared__ float part2[8][kRedCols];
+  __shared__ float part2[kRedRuns][kRedCols];
   SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
   swarm_ctrl* C = ctrl;
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   part[q][c] = s;
   __syncthreads();
   SWARM_STAMP(30);
-  if (q < 8) {
+  if (q < kRedRuns) {
     float r = part[8 * q][c];
 #pragma unroll
     for (int gi = 1; gi < 8; ++gi) r = r + part[8 * q + gi][c];
@@ -146,7 +152,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   if (q == 0 && col <= N_PARAMS) {
     float tot = part2[0][c];
 #pragma unroll
-    for (int gi = 1; gi < 8; ++gi) tot = tot + part2[gi][c];
+    for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
     A.grad[col] = tot;
     // loss of this update (0 when skipped: the TD launch wrote zero slabs)
     if (advance && col == N_PARAMS) C->loss = tot / (float)((size_t)A.batch * A.N);
