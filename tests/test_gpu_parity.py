@@ -438,7 +438,7 @@ def test_training_is_bitwise_deterministic(sw, golden_weights):
 
 @pytest.mark.parametrize("scen,N,graph,conv", [("GoTo", 8, "complete", "gat"), ("ObstacleAvoidance", 12, "knn", "gat"),
                                                ("ObstacleAvoidance", 10, "complete", "gcn"),
-                                               ("Flocking", 8, "complete", "gat")])
+                                               ("Flocking", 8, "complete", "gat"), ("Flocking", 20, "knn", "gat")])
 def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
     """Fused tick (optimizer step deferred into the next act launch, ping-pong buffers)
     == act + td_grad + grad_reduce + adam_step, bit for bit, incl. target syncs."""
@@ -554,8 +554,9 @@ def test_gat3_q_forward_parity(sw, golden_weights, N, graph):
     assert torch.equal(q.argmax(-1)[m], ref.argmax(-1)[m])
 
 
-def test_gat3_q_forward_from_pyg_edge_index(sw, golden_weights):
-    N, G = 6, 7
+@pytest.mark.parametrize("N", [6, 20])
+def test_gat3_q_forward_from_pyg_edge_index(sw, golden_weights, N):
+    G = 7
     flat, P = _gat3(golden_weights, 3)
     model = sw.GCN.from_state_dict(P)
     pos, vel = _rand_state(G, N, 8)
@@ -566,13 +567,16 @@ def test_gat3_q_forward_from_pyg_edge_index(sw, golden_weights):
     assert_close_rel(q, O.gat3_q_forward_edges(P, batch.x, batch.edge_index), 1e-5, "Q(gat3, edge_index)")
 
 
-@pytest.mark.parametrize("N,graph", [(8, "knn"), (5, "complete"), (12, "radius")])
-def test_gat3_flocking_rollout_matches_oracle_ticks(sw, golden_weights, N, graph):
-    """The Flocking checkpoints acting in the Flocking scenario: one swarm_rollout launch vs the
-    oracle's graph -> GAT3 -> argmax -> env.step -> shaped reward, tick by tick (greedy)."""
+@pytest.mark.parametrize("scen,N,graph", [("flocking", 8, "knn"), ("flocking", 5, "complete"),
+                                          ("flocking", 12, "radius"), ("flocking", 24, "knn"),
+                                          ("obstacle_avoidance", 10, "knn")])
+def test_gat3_flocking_rollout_matches_oracle_ticks(sw, golden_weights, scen, N, graph):
+    """The Flocking checkpoints acting (in the Flocking scenario, and in OA: the network does not
+    depend on it): one swarm_rollout launch vs the oracle's graph -> GAT3 -> argmax -> env.step
+    -> reward, tick by tick (greedy)."""
     B, T = 48, 6
     flat, P = _gat3(golden_weights, 1)
-    eng = sw.SwarmEngine("Flocking", N, B, seed=2, params=flat, graph=graph, knn_k=5, radius=0.3, learn=False,
+    eng = sw.SwarmEngine(scen, N, B, seed=2, params=flat, graph=graph, knn_k=5, radius=0.3, learn=False,
                          net="gat3", eps=0.0)
     eng.reset(0)
     torch.cuda.synchronize()
@@ -584,13 +588,14 @@ def test_gat3_flocking_rollout_matches_oracle_ticks(sw, golden_weights, N, graph
     rew = torch.zeros(B, N)
     ok = torch.ones(B, dtype=torch.bool)   # envs whose greedy actions were clear of Q near-ties so far
     for t in range(T):
-        ref = O.act_tick(P, pos, vel, O.SCENARIO_FLOCK, gid, 5, 0.0, 2, t, radius=0.3)
+        ref = O.act_tick(P, pos, vel, SCEN[scen], gid, 5, 0.0, 2, t, radius=0.3)
         ok &= _tie_mask(ref.q).all(-1)
         got = r["traj_pos"][t].cpu()
         assert (got[ok] - ref.step["pos"][ok]).abs().max() <= 1e-5, t
         pos, vel = ref.step["pos"], ref.step["vel"]
         rew += ref.step["rew"]
-    assert ok.float().mean() > 0.8
+    # envs whose every greedy choice so far was clear of a 1e-4 Q near-tie: fewer as N grows
+    assert ok.float().mean() > (0.8 if N <= 12 else 0.3)
     err = (r["reward"].cpu()[ok] - rew[ok]).abs().max()
     assert err <= 1e-3, err   # T summed flocking rewards (x10-shaped differences)
 
