@@ -2,14 +2,16 @@
 tick, GoTo, 8 agents x 1024 envs per GPU (BASELINE.json configs[1]; weak scaling
 to configs[3] = 8192 envs over 8 GPUs).
 
-One step = one training tick of the reference's hot loop (train_gcn_dqn.py:153-178)
-for every env of every rank: GAT Q forward on the complete graph -> ε-greedy
-(ε = 0.05) -> VMAS env.step -> replay push -> TD update on S = 1024 sampled graphs
-per rank (target fwd, online fwd, backward) -> [RCCL all-reduce of the 1,673-float
-gradient] -> clip_grad_norm_ + Adam (+ target sync every 200 ticks) -> episode reset
-every 100 ticks.  Inputs: synthetic reset states (Philox), weights
-data/models/experiment_GoTo-seed_0.pth (committed fixture), replay pre-filled with
-100 acting ticks.  Timed ticks are replayed from captured hipGraphs.
+One step = one training EPISODE of the reference's hot loop (train_gcn_dqn.py:153-178:
+reset_world_at, then max_steps = 100 ticks) for every env of every rank.  One tick:
+GAT Q forward on the complete graph -> ε-greedy (ε = 0.05) -> VMAS env.step -> replay
+push -> TD update on S = 1024 sampled graphs per rank (target fwd, online fwd, backward)
+-> [RCCL all-reduce of the 1,673-float gradient] -> clip_grad_norm_ + Adam (+ target
+sync every 200 ticks).  A 100-tick step keeps the timed region well above launch and
+sync noise at the driver's K (20 steps = 2,000 ticks); `tick_us` reports the spread of
+the per-episode times (HIP events between steps).  Inputs: synthetic reset states
+(Philox), weights data/models/experiment_GoTo-seed_0.pth (committed fixture), replay
+pre-filled with 100 acting ticks.  Each episode's 100 ticks replay one captured hipGraph.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N > 1: torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -89,8 +91,10 @@ def mean_in_degree(args, eng) -> float:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20, help="timed steps (training: episodes of --ticks ticks)")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ticks", type=int, default=100, help="ticks per step = per episode (max_steps, "
+                    "train_gcn_dqn.py:149)")
     ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--scenario", default="GoTo")
@@ -107,7 +111,6 @@ def parse():
     ap.add_argument("--net", default="gcn", choices=("gcn", "gat3"),
                     help="gat3: the Flocking checkpoints' three-layer GAT (acting only, --mode act)")
     ap.add_argument("--batch", type=int, default=None, help="sampled graphs per update per GPU (default = envs)")
-    ap.add_argument("--chunk", type=int, default=20, help="ticks per captured hipGraph")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -153,7 +156,7 @@ def main():
                                 replay_capacity=1_000_000 if args.net == "gcn" else 1, conv=args.conv,
                                 graph=args.graph, knn_k=args.knn_k, radius=args.radius, net=args.net,
                                 learn=args.net == "gcn")
-    max_steps = 100
+    max_steps = args.ticks
     if args.mode == "act":
         return bench_act(args, eng, world, rank, distributed, max_steps)
     # ---- prefill: 100 acting ticks (no learning)
@@ -162,7 +165,6 @@ def main():
         eng.act(push=True, full_out=False)
         eng.advance()
     eng.reset()
-    tick_in_ep = [0]
 
     fused = eng.fused and args.tick == "fused"
 
@@ -172,12 +174,11 @@ def main():
         else:
             eng.train_tick3(full_out=False)
 
-    chunk = max(1, math.gcd(args.steps, args.chunk)) if args.steps else 1
     graph = None
     if not args.no_graph and (not distributed or args.backend == "nccl"):
         tick()                              # eager warm tick (and first RCCL all-reduce) before capture
         try:
-            graph = eng.capture(chunk, tick)
+            graph = eng.capture(max_steps, tick)   # one episode's ticks
         except RuntimeError as e:           # e.g. a collective that refuses stream capture
             print(f"[bench] rank {rank}: hipGraph capture failed ({e}); eager ticks", file=sys.stderr)
             graph = None
@@ -186,34 +187,37 @@ def main():
             torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
             if int(ok.item()) == 0:
                 graph = None
+    stream = torch.cuda.current_stream()
 
-    def run(n):
-        done = 0
-        while done < n:
-            if tick_in_ep[0] >= max_steps:
-                eng.reset()
-                tick_in_ep[0] = 0
-            if graph is not None and n - done >= chunk and tick_in_ep[0] + chunk <= max_steps:
-                graph.replay()
-                done += chunk
-                tick_in_ep[0] += chunk
-            else:
+    def episode():   # one step: reset_world_at, then max_steps ticks
+        eng.reset()
+        if graph is not None:
+            graph.replay()
+        else:
+            for _ in range(max_steps):
                 tick()
-                done += 1
-                tick_in_ep[0] += 1
 
-    run(args.warmup)
+    for _ in range(args.warmup):
+        episode()
     torch.cuda.synchronize()
     if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    run(args.steps)
+    evs[0].record(stream)
+    for i in range(args.steps):
+        episode()
+        evs[i + 1].record(stream)
     torch.cuda.synchronize()
     if distributed:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ep_us = [evs[i].elapsed_time(evs[i + 1]) * 1e3 / max_steps for i in range(args.steps)]
+    tick_spread = ({"median": round(float(np.median(ep_us)), 3), "min": round(min(ep_us), 3),
+                    "max": round(max(ep_us), 3), "per": "episode of %d ticks, HIP events" % max_steps}
+                   if ep_us else None)
     if distributed:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -233,8 +237,9 @@ def main():
         if not replicas:
             raise SystemExit(f"rank {rank}: replicas diverged after {args.steps} ticks")
 
-    value = B * N * world * args.steps / elapsed
-    ms = elapsed / args.steps * 1e3
+    value = B * N * world * args.steps * max_steps / elapsed
+    ms = elapsed / args.steps * 1e3          # per step (episode)
+    tick_ms = ms / max_steps
 
     # ---- per-kernel durations.  Fused tick: a captured chain of KCHAIN real tick launches, each
     #      followed by swarm_ctrl_advance (tick counter, replay slot: every launch publishes and
@@ -266,10 +271,9 @@ def main():
             t_adv = chain_us(eng.advance, 40)
             eng.flush()
             eng.reset()
-            tick_in_ep[0] = 0
             kt["tick_kernel"] = t_pair - t_adv
             kt["ctrl_advance_kernel"] = t_adv
-            kt["grad_reduce_kernel (tick share)"] = ms * 1e3 - kt["tick_kernel"]
+            kt["grad_reduce_kernel (tick share)"] = tick_ms * 1e3 - kt["tick_kernel"]
             assert eng.handoff_errors() == 0, "fused tick: a hand-off wait hit its bound"
         else:
             for name, fn in (("td_kernel", eng.launch_td), ("act_kernel", eng.launch_train_act),
@@ -328,6 +332,8 @@ def main():
                 "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference GoTo seed_0 weights)",
+                "step": f"one training episode: reset + {max_steps} ticks", "us_per_tick": round(tick_ms * 1e3, 3),
+                "tick_us": tick_spread,
                 "config": {"workload": f"{scen} train tick: {N} agents x {B} envs/GPU, {args.conv.upper()}, "
                                        f"{ {'complete': 'complete', 'knn': f'kNN-{args.knn_k}', 'radius': f'radius-{args.radius}'}[args.graph]} graph, "
                                        f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
@@ -349,17 +355,10 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
     registers across ticks).  No collective: N > 1 runs independent replicas."""
     B, N = args.envs, args.agents
 
-    def run(n):
-        done, t_ep = 0, 0
-        eng.reset()
-        while done < n:
-            if t_ep >= max_steps:
-                eng.reset()
-                t_ep = 0
-            m = min(max_steps - t_ep, n - done)
-            eng.rollout(m, tick0=done, eps=0.0)
-            done += m
-            t_ep += m
+    def run(n_episodes):   # one step = one episode: reset, then one max_steps-tick rollout launch
+        for i in range(n_episodes):
+            eng.reset()
+            eng.rollout(max_steps, tick0=i * max_steps, eps=0.0)
 
     run(args.warmup)
     torch.cuda.synchronize()
@@ -401,9 +400,11 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
                 "algorithmic_flops_per_launch": flops, "launch_us": round(t_l * 1e6, 2)}
     if rank == 0:
         g = {"complete": "complete", "knn": f"kNN-{args.knn_k}", "radius": f"radius-{args.radius}"}[args.graph]
-        line = {"metric": "env-steps/sec (agents×envs), acting-only rollout", "value": round(B * N * world * args.steps / elapsed, 1),
+        line = {"metric": "env-steps/sec (agents×envs), acting-only rollout",
+                "value": round(B * N * world * args.steps * max_steps / elapsed, 1),
                 "unit": "agent-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+                "step": f"one episode: reset + {max_steps}-tick rollout launch",
                 "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox resets; reference seed_0 weights)",
                 "config": {"workload": f"{args.scenario} acting-only: {N} agents x {B} envs/GPU, "
                                        f"{'GAT3 (Flocking checkpoints)' if args.net == 'gat3' else args.conv.upper()}, "

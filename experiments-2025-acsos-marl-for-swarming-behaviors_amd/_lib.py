@@ -26,7 +26,7 @@ ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
           -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class SwarmConfig(ctypes.Structure):
@@ -64,7 +64,9 @@ _PROTOS = {
     "swarm_abi_version": (c_int32, []),
     "swarm_n_params": (c_int32, []),
     "swarm_build_info": (ctypes.c_char_p, []),
+    "swarm_state_floats": (c_int64, [POINTER(SwarmConfig)]),
     "swarm_env_reset": (c_int32, [POINTER(SwarmConfig), c_void_p, c_uint32, c_void_p]),
+    "swarm_env_sync_state": (c_int32, [POINTER(SwarmConfig), c_void_p, c_int32, c_void_p]),
     "swarm_env_step": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, POINTER(SwarmActOut), c_void_p]),
     "swarm_build_graph": (c_int32, [POINTER(SwarmConfig), c_void_p, c_void_p, c_void_p]),
     "swarm_edges_to_mult": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
@@ -121,6 +123,21 @@ def load(require_gpu: bool = True):
             raise RuntimeError("libswarm_hip ABI mismatch")
         _lib = lib
     return _lib
+
+
+def load_variant(path: str):
+    """A second build of the library (e.g. build.HODROP_OUT, the hand-off overrun test
+    library) with the same prototypes, loaded beside the main one; for tests."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.swarm_abi_version() != ABI_VERSION:
+        raise RuntimeError("libswarm_hip ABI mismatch")
+    return lib
 
 
 def check(rc: int, what: str):

@@ -35,14 +35,18 @@ def up_to_date() -> bool:
 
 
 STAMPS_OUT = os.path.join(HERE, "libswarm_hip_stamps.so")
+# test-only variant: every fused-tick hand-off wait overruns at once (tests of the drop path)
+HODROP_OUT = os.path.join(HERE, "libswarm_hip_hodrop.so")
+VARIANTS = {"main": (OUT, []), "stamps": (STAMPS_OUT, ["-DSWARM_STAMPS=1"]),
+            "hodrop": (HODROP_OUT, ["-DSWARM_HO_FORCE_DROP=1"])}
 
 
-def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> str:
-    """stamps=True builds the diagnostic library (in-kernel s_memtime stamps)."""
-    out = STAMPS_OUT if stamps else OUT
+def build(force: bool = False, verbose: bool = True, stamps: bool = False, variant: str = "main") -> str:
+    """stamps=True (or variant="stamps") builds the diagnostic library (in-kernel s_memtime
+    stamps); variant="hodrop" the hand-off overrun test library."""
+    out, extra = VARIANTS["stamps" if stamps else variant]
     if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _deps()):
         return out
-    extra = ["-DSWARM_STAMPS=1"] if stamps else []
     # one hipcc process per translation unit (in parallel), then one link
     objs = [f"{out}.{os.path.splitext(src)[0]}.o" for src in SOURCES]
     cflags = [f for f in FLAGS if f != "-shared"]
@@ -63,4 +67,5 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> st
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)
+    v = next((a[len("--variant="):] for a in sys.argv if a.startswith("--variant=")), "main")
+    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv, variant=v)

@@ -56,6 +56,30 @@ __global__ void reset_kernel(int B, int N, int scenario, int flags, uint32_t k0,
   reinterpret_cast<float4*>(state)[gid] = make_float4(cx + ox, cy + oy, 0.0f, 0.0f);
 }
 
+// ---------------------------------------------------------------- scenario state (Flocking)
+// previous_distance_to_agents of every agent, from the positions in `state`, into the [B][N]
+// floats after it.  fresh != 0: as reset_world_at leaves it (flocking_scenario.py:93-122): the
+// loop sets agent i's position and measures it in the same iteration, so agents j > i are still
+// where VMAS's World.reset put them (zeroed, before reset_world_at runs); fresh == 0: as a
+// reward call leaves it (:151-164), every agent at its current position.  Same operation order
+// as act_body's post-step spread.
+__global__ void flock_state_kernel(int B, int N, int fresh, float* __restrict__ state) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = gid / N, i = gid - env * N;
+  if (env >= B) return;
+  const float4* st = reinterpret_cast<const float4*>(state) + (size_t)env * N;
+  const float4 me = st[i];
+  float s = 0.0f;
+  for (int j = 0; j < N; ++j) {
+    if (j == i) continue;
+    float qx = 0.0f, qy = 0.0f;
+    if (!fresh || j < i) { const float4 o = st[j]; qx = o.x; qy = o.y; }
+    const float b = norm2(me.x - qx, me.y - qy) - kFlockDesired;
+    s = s + b * b;
+  }
+  state[(size_t)B * N * 4 + gid] = (s / (float)(N - 1)) * kFlockShaping;
+}
+
 // ---------------------------------------------------------------- graph build
 template <int NS>
 __global__ __launch_bounds__(64) void graph_kernel(ActArgs A, uint8_t* __restrict__ mult_out) {
@@ -200,6 +224,24 @@ int swarm_env_reset(const swarm_config* cfg, float* state, uint32_t episode, voi
   hipLaunchKernelGGL(reset_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, cfg->n_envs,
                      cfg->n_agents, cfg->scenario, cfg->flags, (uint32_t)(cfg->seed & 0xFFFFFFFFu),
                      (uint32_t)(cfg->seed >> 32), cfg->env_offset, episode, state);
+  if (cfg->scenario == SWARM_FLOCKING)
+    hipLaunchKernelGGL(flock_state_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, cfg->n_envs,
+                       cfg->n_agents, 1, state);
+  return (int)hipGetLastError();
+}
+
+int64_t swarm_state_floats(const swarm_config* cfg) {
+  if (int e = check_cfg(cfg)) return e;
+  const int64_t n = (int64_t)cfg->n_envs * cfg->n_agents;
+  return n * (cfg->scenario == SWARM_FLOCKING ? 5 : 4);
+}
+
+int swarm_env_sync_state(const swarm_config* cfg, float* state, int32_t fresh, void* stream) {
+  if (int e = check_cfg(cfg)) return e;
+  const int n = cfg->n_envs * cfg->n_agents;
+  if (n == 0 || cfg->scenario != SWARM_FLOCKING) return 0;
+  hipLaunchKernelGGL(flock_state_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, cfg->n_envs,
+                     cfg->n_agents, fresh ? 1 : 0, state);
   return (int)hipGetLastError();
 }
 

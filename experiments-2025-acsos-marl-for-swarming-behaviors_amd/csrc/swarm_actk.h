@@ -102,6 +102,12 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
     }
   }
+  // Flocking: the scenario's per-agent previous_distance_to_agents (flocking_scenario.py:110-122,
+  // 163-164), kept after the [B][N][4] state as [B][N] floats (swarm_hip.h, swarm_env_reset)
+  float* fl_prev = (SCEN == SWARM_FLOCKING && MODE != MODE_Q) ? state + (size_t)B * N * 4 : nullptr;
+  float spread[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) spread[ct] = (fl_prev && valid[ct] && p == 0) ? fl_prev[node[ct]] : 0.0f;
   // the whole control block in registers, loaded once and up front (two scalar lines in
   // flight together instead of dependent loads behind branches)
   swarm_ctrl cc = {};
@@ -302,25 +308,26 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     wave_lds_sync();
     float rf = 0.0f;   // flocking: the collective reward
     if (SCEN == SWARM_FLOCKING) {
-      // every agent's term from its pre-step (sm.px/py) and post-step (sm.aux/aux2) distances;
-      // the scenario's "previous" values are exactly the pre-step ones (flocking_scenario.py:102-122, 140-142, 163-164)
+      // every agent's term from its post-step distances (sm.aux/aux2) and the scenario's stored
+      // values: the goal term's equals the pre-step distance (set at reset from the new
+      // position, flocking_scenario.py:102-107, then by every reward call :140-142); the
+      // spread's is carried in `spread` (reset loop value after a reset, :110-122; :163-164)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const int n = 16 * ct + c;
         if (n < NS && p == 0) {
           const float dpre = norm2(px[ct] - kGoalX, py[ct] - kGoalY);
-          float spre = 0.0f, spost = 0.0f, cnt = 0.0f;
+          float spost = 0.0f, cnt = 0.0f;
           for (int j = 0; j < N; ++j) {
             if (j == n) continue;
-            const float a = norm2(px[ct] - sm.px[j], py[ct] - sm.py[j]) - kFlockDesired;
             const float bn = norm2(o[ct].px - sm.aux[j], o[ct].py - sm.aux2[j]);
             const float b = bn - kFlockDesired;
-            spre = spre + a * a;
             spost = spost + b * b;
             if ((bn - kRadius) - kRadius <= kFlockContact) cnt = cnt + 1.0f;   // World.get_distance
           }
           const float others = (float)(N - 1);   // torch mean over the N - 1 other agents
-          const float d_pre = (spre / others) * kFlockShaping, d_post = (spost / others) * kFlockShaping;
+          const float d_pre = spread[ct], d_post = (spost / others) * kFlockShaping;
+          spread[ct] = d_post;
           float rg = dpre * kFlockShaping - o[ct].dgoal * kFlockShaping;               // :140-141
           if (o[ct].dgoal < kRadius) rg = rg + kFlockGoalBonus;                      // on_goal :138, 146-147
           const float term = (rg + (-cnt)) + (d_pre - d_post);                       // :128-129
@@ -412,6 +419,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   for (int ct = 0; ct < CT; ++ct) {
     if (valid[ct] && p == 0) {
       reinterpret_cast<float4*>(state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+      if (fl_prev) fl_prev[node[ct]] = spread[ct];
       if (MODE == MODE_ROLLOUT) {
         if (A.out.reward) A.out.reward[node[ct]] = rew_sum[ct];
         if (A.out.obs) {

@@ -51,6 +51,7 @@ struct TdLds {
   };
   float y[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];
   int act[kTdRows];
+  int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
   __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
 };
@@ -112,7 +113,48 @@ struct TdFused {
   const unsigned long long* ho_rec;   // [B][ho_stride_granules(N)] tagged hand-off records
   uint32_t* ho_err;                   // bounded-wait overruns (0 in a correct run)
 };
-constexpr int kHoSpinLimit = 1 << 18;   // polls (with s_sleep) before a hand-off wait gives up
+#ifndef SWARM_HO_SPIN_LIMIT
+#define SWARM_HO_SPIN_LIMIT (1 << 18)
+#endif
+#ifndef SWARM_HO_FORCE_DROP
+#define SWARM_HO_FORCE_DROP 0
+#endif
+constexpr int kHoSpinLimit = SWARM_HO_SPIN_LIMIT;   // polls (with s_sleep) before a hand-off wait gives up
+// test builds only (libswarm_hip_hodrop.so): every hand-off wait overruns at once
+constexpr bool kHoForceDrop = SWARM_HO_FORCE_DROP != 0;
+
+// A hand-off wait that overruns drops the graphs it waited for: their nodes become padding
+// (no TD error, no gradient, no loss), so the update is the mean over the S*N batch nodes with
+// those graphs' terms zero, never one computed from a stale granule.  The overrun is counted in
+// the workspace's error word (SwarmEngine.handoff_errors; DQNTrainer raises on it).  Node slot
+// 16 ct + c belongs to graph (16 ct + c) / GS: with GS < 16 the lanes of its column group
+// (c / GS, all four row groups) in one ct; GS = 16 one whole ct; GS = 32 both.
+template <int NS, int GS>
+__device__ inline void drop_overrun(const bool (&okc)[DGeom<NS>::CT], bool (&drop)[DGeom<NS>::CT],
+                                    bool (&nv)[DGeom<NS>::CT], int c) {
+  constexpr int CT = DGeom<NS>::CT;
+  bool bad[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(!okc[ct]);
+    if constexpr (GS < 16) {
+      const unsigned long long cols = (((1ull << GS) - 1ull) << (GS * (c / GS))) * 0x0001000100010001ull;
+      bad[ct] = (m & cols) != 0ull;
+    } else {
+      bad[ct] = m != 0ull;
+    }
+  }
+  if constexpr (GS > 16) {   // one graph over every ct of the wave
+    bool any = false;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) any = any || bad[ct];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) bad[ct] = any;
+  }
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+    if (bad[ct]) { drop[ct] = true; nv[ct] = false; }
+}
 
 template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
@@ -216,6 +258,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   SWARM_STAMP(1);
   const bool waited = FUSED && __builtin_amdgcn_ballot_w64(wait) != 0;
+  bool live_drop[CT];   // this wave's graph was dropped after a hand-off overrun
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) live_drop[ct] = false;
   if (FUSED) {   // the pending optimizer step (train_gcn_dqn.py:125-133), as every acting block does;
                  // done before any hand-off wait so that none of it follows the wait
     const bool pending = cc.trained != 0u;
@@ -229,8 +274,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       const uint32_t tag = cc.tick + 1u;
       for (int spin = 0;; ++spin) {
         bool ok = true;
+        bool okc[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
+          okc[ct] = true;
           if (ho[ct]) {
             const unsigned long long* rec = X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
             const int j = min(jl[ct], N - 1);
@@ -238,16 +285,18 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
             const unsigned long long g0 = ld_granule(sp), g1 = ld_granule(sp + 1), g2 = ld_granule(sp + 2),
                                      g3 = ld_granule(sp + 3);
             const unsigned long long g4 = online ? ld_granule(rec + 9 * N + j) : ((unsigned long long)tag << 32);
-            ok = ok && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag && (uint32_t)(g2 >> 32) == tag &&
-                 (uint32_t)(g3 >> 32) == tag && (uint32_t)(g4 >> 32) == tag;
+            okc[ct] = !kHoForceDrop && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag &&
+                      (uint32_t)(g2 >> 32) == tag && (uint32_t)(g3 >> 32) == tag && (uint32_t)(g4 >> 32) == tag;
+            ok = ok && okc[ct];
             st[ct] = make_float4(__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1),
                                  __uint_as_float((uint32_t)g2), __uint_as_float((uint32_t)g3));
             if (online) act[ct] = nv[ct] ? (int)(uint32_t)g4 : 0;
           }
         }
         if (!__builtin_amdgcn_ballot_w64(!ok)) break;
-        if (spin >= kHoSpinLimit) {   // never in a correct run: count it, go on with what is there
+        if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
           if (lane == 0) atomicAdd(X.ho_err, 1u);
+          drop_overrun<NS, GS>(okc, live_drop, nv, c);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -281,18 +330,22 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     const uint32_t tag = cc.tick + 1u;
     for (int spin = 0;; ++spin) {
       bool ok = true;
+      bool okc[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        if (ho[ct]) {
+        okc[ct] = true;
+        if (ho[ct] && !live_drop[ct]) {
           const unsigned long long g = ld_granule(X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) +
                                                   8 * N + min(jl[ct], N - 1));
-          ok = ok && (uint32_t)(g >> 32) == tag;
+          okc[ct] = !kHoForceDrop && (uint32_t)(g >> 32) == tag;
+          ok = ok && okc[ct];
           rew[ct] = __uint_as_float((uint32_t)g);
         }
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
-      if (spin >= kHoSpinLimit) {
+      if (kHoForceDrop || spin >= kHoSpinLimit) {
         if (lane == 0) atomicAdd(X.ho_err, 1u);
+        drop_overrun<NS, GS>(okc, live_drop, nv, c);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -304,7 +357,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       float qmax = F.q[ct][0];
 #pragma unroll
       for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[ct][a]);
-      if (16 * ct + c < NS) TB.y[row0 + 16 * ct + c] = nv[ct] ? rew[ct] + A.gamma * qmax : 0.0f;
+      if (16 * ct + c < NS) {
+        TB.y[row0 + 16 * ct + c] = nv[ct] ? rew[ct] + A.gamma * qmax : 0.0f;
+        if (FUSED) TB.tdrop[row0 + 16 * ct + c] = live_drop[ct] ? 1 : 0;
+      }
     }
   }
   if (!online && !waited) __builtin_amdgcn_s_setprio(0);
@@ -319,6 +375,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c, nn = min(n, NS - 1);
+      if (FUSED && TB.tdrop[row0 + nn]) nv[ct] = false;   // the target wave dropped the graph
       float qa = F.q[ct][0];
 #pragma unroll
       for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? F.q[ct][a] : qa;

@@ -187,6 +187,7 @@ class DQNTrainer:
             epsilon = max(min_epsilon, initial_epsilon * np.exp(-epsilon_decay * episode))
             average_loss = float(self._acc_loss.item()) / max_steps
             ep_reward = float(self._acc_reward.item())
+            eng.check_handoffs()   # an overrun hand-off dropped TD graphs: fail loudly (one 4-byte read)
             self.episode_losses.append(average_loss)
             self.rewards_buffer.append(torch.tensor(ep_reward))
             if (episode + 1) % 10 == 0:

@@ -129,7 +129,13 @@ class SwarmEngine:
                                update_target_every, world_size, 0)
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.state = torch.zeros(n_envs, n_agents, 4, **f32)
+        # [B][N][4] pos.xy, vel.xy; Flocking keeps its per-agent previous_distance_to_agents after
+        # it (swarm_state_floats), as `scenario_state` [B][N]
+        nst = int(self.lib.swarm_state_floats(ctypes_ref(self.cfg)))
+        check(min(nst, 0), "swarm_state_floats")
+        self._state_buf = torch.zeros(max(nst, 1), **f32)
+        self.state = self._state_buf[: n_envs * n_agents * 4].view(n_envs, n_agents, 4)
+        self.scenario_state = self._state_buf[n_envs * n_agents * 4: nst].view(n_envs, n_agents)
         n_par = _lib.GAT3_N_PARAMS if net == "gat3" else N_PARAMS
         if params is None:
             if net == "gat3":
@@ -204,6 +210,13 @@ class SwarmEngine:
         check(self.lib.swarm_env_reset(ctypes_ref(self.cfg), ptr(self.state), ep, stream_ptr()), "swarm_env_reset")
         self.episode = ep + 1
         return self.state
+
+    def set_state(self, pos: torch.Tensor, vel: torch.Tensor, fresh: bool = False):
+        """Write agent positions/velocities [B, N, 2] and bring the scenario's per-agent state in
+        line with them (Flocking): fresh=True as right after reset_world_at, else as after a step."""
+        self.state.copy_(torch.cat([pos, vel], -1).to(self.state))
+        check(self.lib.swarm_env_sync_state(ctypes_ref(self.cfg), ptr(self.state), int(fresh), stream_ptr()),
+              "swarm_env_sync_state")
 
     def env_step(self, actions: torch.Tensor, out: Optional[SwarmActOut] = None):
         a = actions.to(device=self.device, dtype=torch.int32).contiguous()
@@ -302,6 +315,16 @@ class SwarmEngine:
         if self.tick_ws is None:
             return 0
         return int(self.tick_ws[:4].view(torch.int32).item())   # the workspace's first word
+
+    def check_handoffs(self):
+        """Raise if any fused-tick hand-off wait overran since the workspace was zeroed.  An
+        overrun drops the graphs it waited for from that tick's TD batch (their terms are zero,
+        the mean stays over S*N nodes), so training never consumes a stale transition; this
+        makes the event loud.  One 4-byte device read: call it once per episode."""
+        n = self.handoff_errors()
+        if n:
+            raise RuntimeError(f"fused training tick: {n} hand-off wait(s) overran their bound; the graphs they "
+                               "waited for were dropped from their TD batches (use train_tick3 on this device)")
 
     def train_tick(self, full_out: bool = False):
         """Fused training tick: 2 launches (+ an RCCL all-reduce when world_size > 1), or the

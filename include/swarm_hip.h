@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 5
+#define SWARM_ABI_VERSION 6
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
@@ -145,9 +145,21 @@ int swarm_abi_version(void);
 int swarm_n_params(void);                 /* 1673 */
 const char* swarm_build_info(void);
 
+/* Environment state: [B][N][4] floats (pos.xy, vel.xy) for every scenario.  SWARM_FLOCKING
+ * keeps per-agent scenario state after it: [B][N] floats of previous_distance_to_agents
+ * (flocking_scenario.py:110-122 at reset, :163-164 per reward call), which every entry point
+ * that steps the env reads and writes.  swarm_state_floats gives the buffer size. */
+int64_t swarm_state_floats(const swarm_config* cfg);
+
 /* Reset: reset_world_at + generate_grid (go_to_position_scenario.py:52-106,
- * obstacle_avoidance_scenario.py:63-133) for all B envs; state [B][N][4]. */
+ * obstacle_avoidance_scenario.py:63-133, flocking_scenario.py:86-122) for all B envs. */
 int swarm_env_reset(const swarm_config* cfg, float* state, uint32_t episode, void* stream);
+
+/* Recompute the scenario state that follows [B][N][4] (Flocking; a no-op otherwise) from the
+ * positions in `state`, after a caller wrote them: fresh != 0 as reset_world_at leaves it (the
+ * reset loop measures agent i against the new positions of agents < i and the zeroed ones of
+ * agents > i, flocking_scenario.py:93-122), fresh == 0 as a step's reward call leaves it. */
+int swarm_env_sync_state(const swarm_config* cfg, float* state, int32_t fresh, void* stream);
 
 /* VMAS Environment.step for discrete actions (call sites train_gcn_dqn.py:169,
  * simulator.py:68): decode, holonomic force, sphere collisions, drag/Euler,

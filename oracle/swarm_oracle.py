@@ -130,8 +130,14 @@ def pair_force(pos_a: torch.Tensor, pos_b: torch.Tensor, dist_min: float = 2 * S
     return force
 
 
-def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenario: int):
+def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenario: int,
+             prev_spread: torch.Tensor | None = None):
     """One VMAS step for [B, N] agents.  Returns dict of new state, rewards and metrics.
+
+    Flocking keeps per-agent state (``previous_distance_to_agents``): ``prev_spread`` [B, N]
+    is its value before the step (``flocking_reset_spread`` right after a reset; None = the
+    shaped spread of ``pos``, which is what every later step stores), and the returned
+    dict's ``spread`` is the value after it.
 
     Force summation order follows VMAS: force = 0 + u, then the obstacle pair
     (landmarks precede agents in ``world.entities``), then agent pairs (a<b) in
@@ -163,7 +169,7 @@ def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenar
     goal = f32(GOAL)
     dist_goal = vector_norm2(pos_new - goal)                    # [B, N]
     if scenario == SCENARIO_FLOCK:
-        rew, hits = flocking_reward(pos, pos_new)
+        rew, hits, spread = flocking_reward(pos, pos_new, prev_spread)
         d_obs = torch.zeros(B, N)
     elif scenario == SCENARIO_GOTO:
         r = torch.zeros(B)
@@ -179,8 +185,11 @@ def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenar
         rew = -dist_goal + 2.5 * obst_rew
         hits = (d_obs <= 0.2).sum(dim=1).to(torch.float32)                       # :318-321
     avg_dist = torch.mean(dist_goal, dim=1)
-    return dict(pos=pos_new, vel=vel_new, force=force, rew=rew, dist_goal=dist_goal,
-                avg_dist=avg_dist, hits=hits, d_obs=d_obs)
+    out = dict(pos=pos_new, vel=vel_new, force=force, rew=rew, dist_goal=dist_goal,
+               avg_dist=avg_dist, hits=hits, d_obs=d_obs)
+    if scenario == SCENARIO_FLOCK:
+        out["spread"] = spread
+    return out
 
 
 def _flock_agent_spread(pos: torch.Tensor, i: int) -> torch.Tensor:
@@ -191,17 +200,38 @@ def _flock_agent_spread(pos: torch.Tensor, i: int) -> torch.Tensor:
     return (d - FLOCK_DESIRED).pow(2).mean(-1) * FLOCK_SHAPING
 
 
-def flocking_reward(pos: torch.Tensor, pos_new: torch.Tensor):
+def flocking_reset_spread(pos: torch.Tensor) -> torch.Tensor:
+    """``previous_distance_to_agents`` as ``reset_world_at`` leaves it (flocking_scenario.py:93-122).
+
+    The reset loop places agent i and computes its spread in the same iteration, so agents
+    j < i are already at their new positions while agents j > i are still where VMAS's
+    ``env_reset_world_at`` put them: ``World.reset`` zeroes every entity state before the
+    scenario's ``reset_world_at`` runs (VMAS 1.4.0), i.e. the origin.  [B, N] fp32."""
+    B, N, _ = pos.shape
+    out = torch.zeros(B, N)
+    zero = torch.zeros(B, 2)
+    for i in range(N):
+        d = torch.stack([vector_norm2(pos[:, i] - (pos[:, j] if j < i else zero)) for j in range(N) if j != i], dim=1)
+        out[:, i] = (d - FLOCK_DESIRED).pow(2).mean(-1) * FLOCK_SHAPING
+    return out
+
+
+def flocking_reward(pos: torch.Tensor, pos_new: torch.Tensor, prev_spread: torch.Tensor | None = None):
     """FlockingScenario.reward (flocking_scenario.py:124-176) for [B, N] agents.
 
-    The scenario keeps ``previous_distance_to_goal`` / ``previous_distance_to_agents``
-    per agent; both are exactly the shaped values of the pre-step positions (set at reset,
-    :102-122, and by the previous step's reward), so they are recomputed from ``pos``.
+    The scenario keeps ``previous_distance_to_goal`` / ``previous_distance_to_agents`` per
+    agent.  The goal term's stored value is always the shaped distance of the pre-step
+    position (set at reset :102-107 from the agent's new position, then by every reward call
+    :140-142), so it is recomputed from ``pos``.  The spread's stored value is the previous
+    reward call's (:163-164) except on the first step after a reset, where it is
+    ``flocking_reset_spread``'s mixed old/new value: the caller passes it as ``prev_spread``
+    (None = recompute from ``pos``, the later steps' value).
     ``if agent.on_goal`` only works at B=1 in the reference; this is its batched form.
-    Returns (collective reward broadcast to [B, N], contact count per env)."""
+    Returns (collective reward broadcast to [B, N], contact count per env, spread after [B, N])."""
     B, N, _ = pos.shape
     goal = f32(GOAL)
     total, contacts = None, torch.zeros(B)
+    spread = torch.zeros(B, N)
     for i in range(N):
         d_now = vector_norm2(pos_new[:, i] - goal)
         pos_rew = vector_norm2(pos[:, i] - goal) * FLOCK_SHAPING - d_now * FLOCK_SHAPING
@@ -211,14 +241,17 @@ def flocking_reward(pos: torch.Tensor, pos_new: torch.Tensor):
             if j != i:   # World.get_distance(agent, other) <= min_collision_distance
                 gd = (vector_norm2(pos_new[:, i] - pos_new[:, j]) - SPHERE_RADIUS) - SPHERE_RADIUS
                 cnt = cnt + (gd <= FLOCK_CONTACT).to(torch.float32)
-        dist_rew = _flock_agent_spread(pos, i) - _flock_agent_spread(pos_new, i)
+        before = _flock_agent_spread(pos, i) if prev_spread is None else prev_spread[:, i]
+        spread[:, i] = _flock_agent_spread(pos_new, i)
+        dist_rew = before - spread[:, i]
         term = (r_goal + (-cnt)) + dist_rew
         total = term if total is None else total + term
         contacts = contacts + cnt
-    return total.unsqueeze(1).expand(B, N).clone(), contacts
+    return total.unsqueeze(1).expand(B, N).clone(), contacts, spread
 
 
-def flocking_reward_scale(pos: torch.Tensor, pos_new: torch.Tensor) -> torch.Tensor:
+def flocking_reward_scale(pos: torch.Tensor, pos_new: torch.Tensor,
+                          prev_spread: torch.Tensor | None = None) -> torch.Tensor:
     """[B] sum of the magnitudes the flocking reward is a difference of (shaped goal distances
     and spreads, before and after the step).  The reward cancels most of it, so its fp32
     rounding is bounded relative to this scale, not to the reward itself."""
@@ -228,6 +261,8 @@ def flocking_reward_scale(pos: torch.Tensor, pos_new: torch.Tensor) -> torch.Ten
     for i in range(N):
         for p in (pos, pos_new):
             s += (vector_norm2(p[:, i] - goal) * FLOCK_SHAPING).double() + _flock_agent_spread(p, i).double()
+        if prev_spread is not None:
+            s += prev_spread[:, i].double()
     return s
 
 
@@ -591,7 +626,8 @@ def graph_multiplicity(pos, graph: int, k: int = 0, radius: float = 0.0) -> torc
 
 
 def act_tick(params: dict, pos, vel, scenario: int, graph: int, k: int, eps: float,
-             seed: int, tick: int, conv: str = "gat", env_offset: int = 0, radius: float = 0.0) -> TickOut:
+             seed: int, tick: int, conv: str = "gat", env_offset: int = 0, radius: float = 0.0,
+             prev_spread=None) -> TickOut:
     B, N, _ = pos.shape
     x = node_features(pos, vel)
     mult = graph_multiplicity(pos, graph, k, radius)
@@ -602,7 +638,7 @@ def act_tick(params: dict, pos, vel, scenario: int, graph: int, k: int, eps: flo
     else:
         q = gcn_conv_dense(params, x, mult)
     act, explore, greedy = egreedy(q, eps, seed, tick, env_offset)
-    step = env_step(pos, vel, act, scenario)
+    step = env_step(pos, vel, act, scenario, prev_spread)
     return TickOut(q=q, actions=act, explore=explore, greedy=greedy, step=step, mult=mult)
 
 

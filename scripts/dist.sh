@@ -11,6 +11,6 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 $R --nproc-per-node 1 --master-port 29512 bench.py --gpus 1 --force-dist --no-graph $A > gpurun_out/dist_rccl1_eager.log 2>&1
 rc=$?; echo "rccl1 eager rc=$rc"; tail -1 gpurun_out/dist_rccl1_eager.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 $R --nproc-per-node 2 --master-port 29513 bench.py --gpus 2 --backend gloo --steps 40 $A > gpurun_out/dist_gloo2.log 2>&1
+timeout -k 10 300 $R --nproc-per-node 2 --master-port 29513 bench.py --gpus 2 --backend gloo --steps 2 --ticks 20 $A > gpurun_out/dist_gloo2.log 2>&1
 rc=$?; echo "gloo2 rc=$rc"; tail -1 gpurun_out/dist_gloo2.log
 exit $rc

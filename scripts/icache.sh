@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/icache}
 mkdir -p $OUT
-ARGS="--steps 50 --warmup 5 --no-cpu-baseline --no-kernel-timing"
+ARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-kernel-timing"
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_IFETCH SQ_IFETCH_LEVEL SQ_WAIT_ANY" \
            "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ"; do

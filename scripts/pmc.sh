@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
 mkdir -p $OUT
-ARGS=${BENCH_ARGS:-"--steps 50 --warmup 5 --no-cpu-baseline --no-kernel-timing"}
+ARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --no-kernel-timing"}
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python bench.py --steps 400 --warmup 20 --no-cpu-baseline > gpurun_out/bench_head.log 2>&1
+timeout -k 10 300 python bench.py --steps 40 --warmup 3 --no-cpu-baseline > gpurun_out/bench_head.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_head.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 560 python -u tools/sweep.py gpurun_out/sweep.jsonl > gpurun_out/sweep.log 2>&1

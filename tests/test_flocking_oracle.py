@@ -1,7 +1,9 @@
-"""Flocking scenario (src/scenarios/flocking_scenario.py) in the oracle: the stateless
-restatement (``flocking_reward`` recomputes the scenario's "previous" values from the
-pre-step positions) against a stateful restatement that keeps them per agent exactly as the
-scenario does (:102-122 at reset, :140-142 / :163-164 on every reward call), over rollouts.
+"""Flocking scenario (src/scenarios/flocking_scenario.py) in the oracle: the restatement
+(``flocking_reward`` recomputes the goal term's "previous" value from the pre-step positions and
+carries the spread's as explicit state, ``flocking_reset_spread`` after a reset) against a
+stateful restatement that replays the scenario's own call sequence: the reset loop (:93-122,
+agent i measured against the new positions of agents < i and the zeroed ones of agents > i)
+and every reward call (:140-142, :163-164), over rollouts that start at a reset.
 Parity unpinned against the reference itself: it records no Flocking trajectories."""
 import math
 
@@ -15,10 +17,16 @@ class _StatefulFlocking:
     ``if agent.on_goal`` written as a where)."""
 
     def __init__(self, pos):
+        """reset_world_at (:93-122) on states VMAS's World.reset has just zeroed: the loop sets
+        agent i's position, then measures it against the current positions of all agents."""
         self.N = pos.shape[1]
         goal = O.f32(O.GOAL)
-        self.prev_goal = [torch.linalg.vector_norm(pos[:, i] - goal, dim=1) * 10.0 for i in range(self.N)]
-        self.prev_agents = [self._spread(pos, i) for i in range(self.N)]
+        cur = torch.zeros_like(pos)   # World.reset: every entity at the origin
+        self.prev_goal, self.prev_agents = [], []
+        for i in range(self.N):
+            cur[:, i] = pos[:, i]                                   # agent.set_pos
+            self.prev_goal.append(torch.linalg.vector_norm(cur[:, i] - goal, dim=1) * 10.0)
+            self.prev_agents.append(self._spread(cur, i))
 
     def _spread(self, pos, i):
         d = torch.stack([torch.linalg.vector_norm(pos[:, i] - pos[:, j], dim=-1)
@@ -50,22 +58,44 @@ def _rollout(N, B, T, seed):
     g = torch.Generator().manual_seed(seed)
     c = O.reset_centres(O.SCENARIO_FLOCK, B, seed, 0, shared=False)
     pos = O.grid_positions(c, N)
-    pos = pos + torch.randn(pos.shape, generator=g) * 0.02
     vel = torch.zeros(B, N, 2)
     ref = _StatefulFlocking(pos)
+    spread = O.flocking_reset_spread(pos)
+    assert torch.allclose(spread, torch.stack(ref.prev_agents, 1), rtol=0, atol=1e-4)
     for t in range(T):
         acts = torch.randint(0, 9, (B, N), generator=g)
-        out = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK)
+        out = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK, prev_spread=spread)
         want = ref.reward(out["pos"])
-        assert torch.allclose(out["rew"][:, 0], want, rtol=0, atol=2e-5), (N, t)
+        assert torch.allclose(out["rew"][:, 0], want, rtol=0, atol=2e-5 * max(1.0, want.abs().max().item())), (N, t)
         assert torch.equal(out["rew"][:, 0], out["rew"][:, -1])
-        pos, vel = out["pos"], out["vel"]
+        if t > 0:   # later steps: the stored spread is the pre-step positions' own (recomputable)
+            assert torch.equal(O.env_step(pos, vel, acts, O.SCENARIO_FLOCK)["rew"], out["rew"])
+        pos, vel, spread = out["pos"], out["vel"], out["spread"]
     return out
 
 
-def test_stateless_reward_equals_stateful_scenario():
+def test_reward_with_carried_spread_equals_stateful_scenario():
     for N, B, T in ((2, 16, 30), (5, 32, 40), (8, 16, 25), (12, 8, 15)):
         _rollout(N, B, T, seed=N)
+
+
+def test_first_step_after_reset_uses_the_reset_loop_spread():
+    """the reset loop measures agent i against agents j > i still at the origin, so
+    the first step's spread term differs from one recomputed on the reset grid.  N = 10 at the
+    mean centre (-1.6, 1.6): the collective reward is ~+215 higher than the recomputed one."""
+    N = 10
+    pos = O.grid_positions(torch.tensor([[-1.6, 1.6]]), N)
+    vel = torch.zeros(1, N, 2)
+    acts = torch.zeros(1, N, dtype=torch.long)
+    ref = _StatefulFlocking(pos)
+    first = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK, prev_spread=O.flocking_reset_spread(pos))
+    naive = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK)
+    want = ref.reward(first["pos"])
+    assert abs(first["rew"][0, 0].item() - want.item()) <= 1e-4 * abs(want.item())
+    gap = first["rew"][0, 0].item() - naive["rew"][0, 0].item()
+    assert 150.0 < gap < 300.0, gap
+    # agent 0 sees only zeroed partners; the last agent sees the whole new grid
+    assert torch.allclose(O.flocking_reset_spread(pos)[:, -1], O._flock_agent_spread(pos, N - 1))
 
 
 def test_goal_bonus_and_contacts():

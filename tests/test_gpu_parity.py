@@ -64,19 +64,21 @@ def _tie_mask(q):
 @pytest.mark.parametrize("N", [1, 2, 5, 8, 12, 29, 32])
 def test_env_step_parity(sw, scen, N):
     B = 96
-    eng = sw.SwarmEngine(scen, N, B, seed=1, learn=False)
     if scen == "flocking" and N == 1:   # its spacing reward averages over the other agents
         with pytest.raises(RuntimeError):
-            eng.env_step(torch.zeros(B, N, dtype=torch.long))
+            sw.SwarmEngine(scen, N, B, seed=1, learn=False)
         return
+    eng = sw.SwarmEngine(scen, N, B, seed=1, learn=False)
     for trial, tight in enumerate((False, True)):
         pos, vel = _rand_state(B, N, 10 + trial, tight=tight)
         acts = torch.randint(0, 9, (B, N), generator=torch.Generator().manual_seed(trial))
-        eng.state.copy_(torch.cat([pos, vel], -1).cuda())
+        eng.set_state(pos, vel)
         eng.env_step(acts)
         torch.cuda.synchronize()
         ref = O.env_step(pos, vel, acts, SCEN[scen])
         st = eng.state.cpu()
+        if scen == "flocking":   # the scenario state after the step: the new positions' spreads
+            assert_close_rel(eng.scenario_state.cpu(), ref["spread"], 1e-6, "spread")
         assert (st[..., 2:] - ref["vel"]).abs().max() <= 1e-6
         assert (st[..., :2] - ref["pos"]).abs().max() <= 1e-6
         _assert_reward(eng.reward.cpu(), ref["rew"], scen, pos, ref["pos"])
@@ -101,6 +103,41 @@ def test_reset_parity(sw, scen, shared):
     st = eng.state.cpu()
     assert (st[..., :2] - ref).abs().max() < 2e-6
     assert torch.equal(st[..., 2:], torch.zeros(B, N, 2))
+
+
+@pytest.mark.parametrize("N", [2, 5, 10, 13])
+def test_flocking_first_step_after_reset(sw, N):
+    """flocking_scenario.py:93-122: reset_world_at measures agent i's spread against the new
+    positions of agents < i and the zeroed ones of agents > i; the first step's
+    reward uses that stored value, later steps the previous step's.  Reset -> 3 env.steps vs the
+    oracle carrying the state."""
+    B = 64
+    eng = sw.SwarmEngine("Flocking", N, B, seed=5, learn=False, eps=1.0, replay_capacity=B)
+    eng.reset(2)
+    torch.cuda.synchronize()
+    st = eng.state.cpu()
+    pos, vel = st[..., :2].clone(), st[..., 2:].clone()
+    spread = O.flocking_reset_spread(pos)
+    assert_close_rel(eng.scenario_state.cpu(), spread, 1e-6, "reset spread")
+    g = torch.Generator().manual_seed(N)
+    for t in range(3):
+        acts = torch.randint(0, 9, (B, N), generator=g)
+        eng.env_step(acts)
+        torch.cuda.synchronize()
+        ref = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK, prev_spread=spread)
+        st = eng.state.cpu()
+        assert (st[..., :2] - ref["pos"]).abs().max() <= 1e-6
+        bound = 2e-7 * O.flocking_reward_scale(pos, ref["pos"], spread)[:, None]
+        assert ((eng.reward.cpu().double() - ref["rew"].double()).abs() <= bound).all(), t
+        if t == 0 and N > 2:   # the reset-loop value moves the first reward
+            naive = O.env_step(pos, vel, acts, O.SCENARIO_FLOCK)["rew"]
+            assert ((naive - ref["rew"]).abs() > 1e-3).all()
+        assert_close_rel(eng.scenario_state.cpu(), ref["spread"], 1e-6, "spread")
+        pos, vel, spread = st[..., :2].clone(), st[..., 2:].clone(), eng.scenario_state.cpu().clone()
+    # set_state(fresh=True) == reset_world_at's stored values for the written positions
+    eng.set_state(pos, vel, fresh=True)
+    torch.cuda.synchronize()
+    assert_close_rel(eng.scenario_state.cpu(), O.flocking_reset_spread(pos), 1e-6, "fresh spread")
 
 
 # ------------------------------------------------------------------ graph build
@@ -264,7 +301,7 @@ def _act_tick_case(sw, golden_weights, scen, N, graph, k, conv):
     eng = sw.SwarmEngine(scen, N, B, seed=11, params=p, graph=graph, knn_k=max(k, 1), eps=0.35,
                          replay_capacity=4 * B, conv=conv, radius=radius)
     pos, vel = _rand_state(B, N, 21, tight=(N == 5))
-    eng.state.copy_(torch.cat([pos, vel], -1).cuda())
+    eng.set_state(pos, vel)
     eng.ctrl[0] = 5   # tick
     eng.act(push=True)
     torch.cuda.synchronize()
@@ -506,6 +543,108 @@ def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, c
     assert slots > 100 or n_cur > 0   # the hand-off path really ran
 
 
+def test_handoff_overrun_drops_the_waiting_graphs(sw, golden_weights):
+    """a fused-tick hand-off wait that overruns its bound must not train on stale
+    granules.  The test library (-DSWARM_HO_FORCE_DROP) makes every wait overrun at once: the
+    graphs drawn from the tick's own slot are dropped (zero terms; the mean stays over S*N
+    nodes), the rest of the batch is exact, the overrun is counted and check_handoffs raises."""
+    from swarm_amd import _lib, build
+    lib = _lib.load_variant(build.HODROP_OUT)
+    B, N, S, slots = 32, 8, 32, 2
+    p = _params(golden_weights, "go_to", 2)
+    eng = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, batch=S, eps=0.3, replay_capacity=slots * B,
+                         update_target_every=1000)
+    assert eng.fused
+    eng.lib = lib
+    eng.reset(0)
+    eng.train_tick()   # tick 0: the ring holds only the slot being written -> every graph waits
+    torch.cuda.synchronize()
+    assert eng.handoff_errors() > 0
+    assert torch.count_nonzero(eng.grad.cpu()) == 0   # gradient and loss column
+    with pytest.raises(RuntimeError, match="hand-off"):
+        eng.check_handoffs()
+    ws = eng.read_ctrl()["write_slot"]
+    eng.train_tick()   # tick 1: slot 0's graphs are read from the ring, slot 1's wait and drop
+    torch.cuda.synchronize()
+    idx = eng.samples.cpu().long()
+    cur = (idx // B) == ws
+    assert cur.any() and (~cur).any()
+    keep = idx[~cur]
+    slot, env = keep // B, keep % B
+    ref_loss, ref_grad, _, _ = O.td_loss_grad(eng.params.cpu(), eng.target.cpu(), eng.rep_s.cpu()[slot, env],
+                                              eng.rep_a.cpu()[slot, env].long(), eng.rep_r.cpu()[slot, env],
+                                              eng.rep_s1.cpu()[slot, env])
+    frac = keep.numel() / S   # the oracle's mean is over the kept nodes only
+    g = eng.grad.cpu()
+    assert_close_rel(g[O.N_PARAMS].item() / (S * N), ref_loss * frac, 1e-5, "loss of the kept graphs")
+    gscale = ref_grad.abs().max().clamp_min(1e-3) * frac
+    assert ((g[:O.N_PARAMS] - ref_grad * frac).abs().max() / gscale).item() < 2e-5
+
+
+def test_trainer_raises_on_handoff_overrun(sw, tmp_path):
+    env = sw.make_env(sw.GoToPositionScenario(), num_envs=4, continuous_actions=False, max_steps=5,
+                      dict_spaces=True, seed=0, n_agents=5)
+    tr = sw.DQNTrainer(env, 0, str(tmp_path / "m"), str(tmp_path / "s"), "GoTo", batch_size=8)
+    assert tr.engine.fused
+    tr.engine.tick_ws[:4].view(torch.int32).fill_(1)   # as if a wait had overrun
+    with pytest.raises(RuntimeError, match="hand-off"):
+        tr.train_model({"epsilon": 0.9, "epsilon_decay": 0.01, "min_epsilon": 0.05, "episodes": 2})
+
+
+def test_two_rank_fused_tick_equals_union_batch(sw, golden_weights):
+    """the product's multi-rank path on one GPU.  Two world_size=2 engines own
+    disjoint env shards (env_offset 0 / B); their fused ticks run as on two ranks and the
+    all-reduce is done by hand where the engine would call RCCL (after swarm_reduce_advance,
+    before the next tick's in-register Adam, which divides by W).  Against one world_size=1
+    engine over all 2B envs whose TD batch is the union of the two ranks' batches: same
+    acting, the union-batch gradient, the same weights after the next tick's optimizer step,
+    and bitwise-identical replicas."""
+    B, N, S, slots = 32, 8, 16, 4
+    p = _params(golden_weights, "go_to", 1)
+    kw = dict(seed=6, params=p, eps=0.25, update_target_every=1000)
+    ra = sw.SwarmEngine("GoTo", N, B, batch=S, replay_capacity=slots * B, env_offset=0, world_size=2, **kw)
+    rb = sw.SwarmEngine("GoTo", N, B, batch=S, replay_capacity=slots * B, env_offset=B, world_size=2, **kw)
+    u = sw.SwarmEngine("GoTo", N, 2 * B, batch=2 * S, replay_capacity=slots * 2 * B, **kw)
+    assert ra.fused and rb.fused
+    for e in (ra, rb, u):
+        e.reset(0)
+        for _ in range(2):   # prefill two slots, no learning
+            e.act(push=True, full_out=False)
+            e.advance()
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([ra.state, rb.state]), u.state)
+
+    def rank_ticks():
+        for e in (ra, rb):
+            e.launch_tick()
+            e.launch_reduce_advance()
+        g = ra.grad + rb.grad            # the all-reduce (SUM) of dist.allreduce_grad_
+        ra.grad.copy_(g)
+        rb.grad.copy_(g)
+
+    for t in range(2):
+        ws = ra.read_ctrl()["write_slot"]
+        rank_ticks()
+        u.act(push=True, full_out=False)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat([ra.state, rb.state]), u.state), t
+        ia, ib = ra.samples.cpu().long(), rb.samples.cpu().long()
+        union = torch.cat([(ia // B) * 2 * B + ia % B, (ib // B) * 2 * B + B + ib % B]).to(torch.int32)
+        assert ((ia // B) == ws).any() or ((ib // B) == ws).any() or t == 0   # hand-offs on the ranks
+        u.td_grad(sample_in=union.cuda())
+        torch.cuda.synchronize()
+        gu, gr = u.grad.cpu(), ra.grad.cpu() * 0.5
+        assert_close_rel(gr[O.N_PARAMS].item(), gu[O.N_PARAMS].item(), 1e-5, "loss sum")
+        assert ((gr[:O.N_PARAMS] - gu[:O.N_PARAMS]).abs().max() / gu[:O.N_PARAMS].abs().max()).item() < 2e-5, t
+        u.adam()
+    for e in (ra, rb):
+        e.flush()
+    torch.cuda.synchronize()
+    assert torch.equal(ra.params, rb.params) and torch.equal(ra.adam_v, rb.adam_v)   # replicas
+    assert (ra.params.cpu() - u.params.cpu()).abs().max().item() < 2e-6
+    assert ra.read_ctrl()["adam_step"] == u.read_ctrl()["adam_step"] == 2
+
+
 def test_graph_capture_replay_equals_eager(sw, golden_weights):
     p = _params(golden_weights, "go_to", 1)
     a = sw.SwarmEngine("GoTo", 8, 128, seed=8, params=p, batch=128, eps=0.1)
@@ -587,8 +726,10 @@ def test_gat3_flocking_rollout_matches_oracle_ticks(sw, golden_weights, scen, N,
     gid = {"complete": O.GRAPH_COMPLETE, "knn": O.GRAPH_KNN, "radius": O.GRAPH_RADIUS}[graph]
     rew = torch.zeros(B, N)
     ok = torch.ones(B, dtype=torch.bool)   # envs whose greedy actions were clear of Q near-ties so far
+    spread = O.flocking_reset_spread(pos) if scen == "flocking" else None   # the reset loop's value
     for t in range(T):
-        ref = O.act_tick(P, pos, vel, SCEN[scen], gid, 5, 0.0, 2, t, radius=0.3)
+        ref = O.act_tick(P, pos, vel, SCEN[scen], gid, 5, 0.0, 2, t, radius=0.3, prev_spread=spread)
+        spread = ref.step.get("spread")
         ok &= _tie_mask(ref.q).all(-1)
         got = r["traj_pos"][t].cpu()
         assert (got[ok] - ref.step["pos"][ok]).abs().max() <= 1e-5, t
@@ -748,7 +889,7 @@ def test_maximum_swarm_and_empty_inputs(sw, golden_weights):
                          1e-5, "Q N=32")
     eng = sw.SwarmEngine("ObstacleAvoidance", N, B, seed=3, params=p, eps=0.3, batch=B, replay_capacity=4 * B)
     assert not eng.fused   # n_agents > 16: the 3-launch tick
-    eng.state.copy_(torch.cat([pos, vel], -1).cuda())
+    eng.set_state(pos, vel)
     eng.ctrl[0] = 2
     eng.act(push=True)
     torch.cuda.synchronize()

@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "sweep.jsonl")
-COMMON = ["--no-cpu-baseline", "--steps", "200", "--warmup", "10"]
+COMMON = ["--no-cpu-baseline", "--steps", "20", "--warmup", "3"]
 
 RUNS = [("C3 OA 12x1024 GAT train", ["--scenario", "ObstacleAvoidance", "--agents", "12"])]
 # C5 per GPU: 4096 envs over 8 GPUs = 512 envs/GPU, N = 5..12, GCN vs GAT
