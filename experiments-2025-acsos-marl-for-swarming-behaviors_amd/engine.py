@@ -135,7 +135,8 @@ class SwarmEngine:
         check(min(nst, 0), "swarm_state_floats")
         self._state_buf = torch.zeros(max(nst, 1), **f32)
         self.state = self._state_buf[: n_envs * n_agents * 4].view(n_envs, n_agents, 4)
-        self.scenario_state = self._state_buf[n_envs * n_agents * 4: nst].view(n_envs, n_agents)
+        self.scenario_state = (self._state_buf[n_envs * n_agents * 4: nst].view(n_envs, n_agents)
+                               if nst > n_envs * n_agents * 4 else None)
         n_par = _lib.GAT3_N_PARAMS if net == "gat3" else N_PARAMS
         if params is None:
             if net == "gat3":
