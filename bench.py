@@ -119,6 +119,10 @@ def parse():
                     "gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: create the process group and run the gradient all-reduce even at 1 rank")
+    ap.add_argument("--allreduce", default="auto", choices=("auto", "peer", "rccl"),
+                    help="gradient all-reduce for N > 1: peer = xGMI stores fused into the slab reduce "
+                         "(swarm_reduce_advance_peer); rccl = torch.distributed all_reduce after it; auto = peer "
+                         "if its setup self-test passes on every rank, else rccl")
     return ap.parse_args()
 
 
@@ -140,6 +144,28 @@ def main():
     if distributed:
         torch.distributed.barrier()
 
+    peer, allreduce = None, None
+    if distributed and args.mode == "train":
+        allreduce = "rccl" if args.backend == "nccl" else args.backend
+        if args.allreduce != "rccl":
+            why = None
+            try:
+                peer = swdist.PeerExchange.connect(pg)
+                ok = peer.selftest()
+            except RuntimeError as e:   # e.g. IPC unavailable
+                why, ok = str(e), False
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                                device="cuda" if args.backend == "nccl" else "cpu")
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            if int(flag.item()) == 1:
+                allreduce = "xGMI peer stores fused into the slab reduce (swarm_reduce_advance_peer)"
+            else:
+                if args.allreduce == "peer":
+                    raise SystemExit(f"rank {rank}: peer all-reduce self-test failed ({why or 'wrong sums'})")
+                print(f"[bench] rank {rank}: peer all-reduce self-test failed ({why or 'wrong sums'}); "
+                      f"falling back to {allreduce}", file=sys.stderr)
+                peer = None
+
     B, N = args.envs, args.agents
     shard = swdist.Shard(rank, world, B)
     S = args.batch or B
@@ -155,7 +181,7 @@ def main():
                                 world_size=world, process_group=pg, update_target_every=200,
                                 replay_capacity=1_000_000 if args.net == "gcn" else 1, conv=args.conv,
                                 graph=args.graph, knn_k=args.knn_k, radius=args.radius, net=args.net,
-                                learn=args.net == "gcn")
+                                learn=args.net == "gcn", peer=peer)
     max_steps = args.ticks
     if args.mode == "act":
         return bench_act(args, eng, world, rank, distributed, max_steps)
@@ -175,7 +201,7 @@ def main():
             eng.train_tick3(full_out=False)
 
     graph = None
-    if not args.no_graph and (not distributed or args.backend == "nccl"):
+    if not args.no_graph and (not distributed or args.backend == "nccl" or peer is not None):
         tick()                              # eager warm tick (and first RCCL all-reduce) before capture
         try:
             graph = eng.capture(max_steps, tick)   # one episode's ticks
@@ -183,7 +209,8 @@ def main():
             print(f"[bench] rank {rank}: hipGraph capture failed ({e}); eager ticks", file=sys.stderr)
             graph = None
         if distributed:                     # every rank runs the same launch mode
-            ok = torch.tensor([1 if graph is not None else 0], device="cuda", dtype=torch.int32)
+            ok = torch.tensor([1 if graph is not None else 0], dtype=torch.int32,
+                              device="cuda" if args.backend == "nccl" else "cpu")
             torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
             if int(ok.item()) == 0:
                 graph = None
@@ -224,6 +251,8 @@ def main():
         elapsed = float(t.item())
     ctrl = eng.read_ctrl()
     assert ctrl["trained"] == 1 and math.isfinite(ctrl["loss"]), ctrl
+    if peer is not None:
+        peer.check()   # an expired exchange wait would have summed a wrong gradient: fail loudly
     replicas = None
     if distributed:
         # data-parallel invariant: after the same all-reduced updates every replica's weights,
@@ -338,8 +367,11 @@ def main():
                                        f"{ {'complete': 'complete', 'knn': f'kNN-{args.knn_k}', 'radius': f'radius-{args.radius}'}[args.graph]} graph, "
                                        f"eps 0.05, TD batch {S} graphs/GPU", "envs_per_gpu": B, "agents": N,
                            "global_envs": B * world, "td_batch_per_gpu": S, "graph": args.graph, "conv": args.conv,
-                           "parallelism": f"env-sharded dp{world}" + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce" if distributed else ""),
+                           "parallelism": f"env-sharded dp{world}" + ("" if not distributed else
+                                          " + xGMI peer grad all-reduce" if peer is not None else
+                                          f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce"),
                            "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
+                           "allreduce": allreduce,
                            "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu,
                 "loss": ctrl["loss"]}

@@ -26,7 +26,7 @@ ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
           -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class SwarmConfig(ctypes.Structure):
@@ -53,6 +53,16 @@ class SwarmAdamCfg(ctypes.Structure):
 
 class SwarmLearner(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("w_cur", "w_nxt", "m_cur", "m_nxt", "v_cur", "v_nxt", "target", "grad")]
+
+
+PEER_MAX = 8
+PEER_HANDLE_BYTES = 64
+PEER_SEQ_WORDS = 256
+
+
+class SwarmPeer(ctypes.Structure):
+    _fields_ = [("world_size", c_int32), ("rank", c_int32), ("recv", c_void_p * PEER_MAX), ("seq", c_void_p),
+                ("err", c_void_p), ("timeout_us", c_uint32), ("pad", c_int32)]
 
 
 # swarm_ctrl is 16 x 4-byte words on the device; field -> word index
@@ -97,6 +107,15 @@ _PROTOS = {
     "swarm_train_tick": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
                                    POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
+    "swarm_peer_buffer_bytes": (c_int64, []),
+    "swarm_peer_alloc": (c_int32, [POINTER(c_void_p)]),
+    "swarm_peer_free": (c_int32, [c_void_p]),
+    "swarm_peer_ipc_handle": (c_int32, [c_void_p, c_void_p]),
+    "swarm_peer_ipc_open": (c_int32, [c_void_p, POINTER(c_void_p)]),
+    "swarm_peer_ipc_close": (c_int32, [c_void_p]),
+    "swarm_reduce_advance_peer": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p,
+                                            POINTER(SwarmLearner), c_int32, c_void_p, POINTER(SwarmPeer), c_void_p]),
+    "swarm_peer_allreduce": (c_int32, [POINTER(SwarmPeer), c_void_p, c_int32, c_void_p]),
     "swarm_host_sample_index": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
     "swarm_host_sample_position": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
 }

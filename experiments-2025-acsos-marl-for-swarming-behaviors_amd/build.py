@@ -8,9 +8,9 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["swarm_act.hip", "swarm_td.hip", "swarm_tick.hip"]
+SOURCES = ["swarm_act.hip", "swarm_td.hip", "swarm_tick.hip", "swarm_peer.hip"]
 HEADERS = ["swarm_actk.h", "swarm_tdk.h", "swarm_common.h", "swarm_knn.h", "swarm_wpg.h", "swarm_dl.h", "swarm_env.h",
-           "swarm_adam.h", "swarm_gat3.h"]
+           "swarm_adam.h", "swarm_gat3.h", "swarm_peer.h"]
 OUT = os.path.join(HERE, "libswarm_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # kernarg preload: the leading 14 kernel-argument dwords arrive in SGPRs at wave start (the

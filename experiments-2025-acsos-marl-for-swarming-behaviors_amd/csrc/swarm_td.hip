@@ -7,6 +7,7 @@
 #include <stdlib.h>
 
 #include "swarm_tdk.h"
+#include "swarm_peer.h"
 
 namespace swarm {
 
@@ -35,6 +36,7 @@ struct ReduceArgs {
   int capacity, B, N, batch;
   swarm_adam_cfg hp;
   uint32_t k0, k1;        // replay-sampling key (seed ^ rank salt)
+  swarm_peer peer;        // PEER = 1: the all-reduce over the ranks' exchange buffers (swarm_peer.h)
 };
 
 // 1024 threads = 16 columns x 64 slab groups (105 column blocks: the 1.7 MB of freshly
@@ -53,11 +55,17 @@ constexpr int kRedGroups = SWARM_RED_GROUPS;
 constexpr int kRedRuns = kRedGroups / 8;   // first combine level: runs of 8 group sums
 static_assert(kRedGroups % 8 == 0 && kRedCols * kRedGroups <= 1024, "reduce geometry");
 constexpr int kRedColBlocks = (N_PARAMS + 1 + kRedCols - 1) / kRedCols;
-// slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start
+static_assert(kRedColBlocks <= kPeerSeqRegion, "peer seq region");
+// slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start.
+// PEER = 1 (swarm_reduce_advance_peer): each column block then exchanges its 16 column sums with
+// the other ranks (swarm_peer.h) and writes grad = their rank-ordered sum: the all-reduce costs
+// one xGMI store + poll inside this launch instead of a collective launch after it.
+template <int PEER>
 __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(const float* slabs, swarm_ctrl* ctrl,
                                                                             int n_slabs, int advance, ReduceArgs A) {
   __shared__ float part[kRedGroups][kRedCols];
   __shared__ float part2[kRedRuns][kRedCols];
+  __shared__ float peer_rv[PEER ? SWARM_PEER_MAX : 1][kRedCols];
   SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
   swarm_ctrl* C = ctrl;
@@ -153,9 +161,19 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     float tot = part2[0][c];
 #pragma unroll
     for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
-    A.grad[col] = tot;
-    // loss of this update (0 when skipped: the TD launch wrote zero slabs)
+    if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
+    else A.grad[col] = tot;
+    // this rank's loss of the update (0 when skipped: the TD launch wrote zero slabs)
     if (advance && col == N_PARAMS) C->loss = tot / (float)((size_t)A.batch * A.N);
+  }
+  if (PEER) {
+    __syncthreads();
+    peer_exchange<kRedCols>(A.peer, 0, blockIdx.x, q, c, col, N_PARAMS + 1, part[0], peer_rv);
+    if (q == 0 && col <= N_PARAMS) {
+      float tot = peer_rv[0][c];
+      for (int w = 1; w < A.peer.world_size; ++w) tot = tot + peer_rv[w][c];
+      A.grad[col] = tot;
+    }
   }
   SWARM_STAMP(31);
   SWARM_RTSTAMP(23);
@@ -315,25 +333,43 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
   if (int e = check_td(cfg, hp)) return e;
   ReduceArgs a = {};
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = grad;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3(kRedColBlocks), dim3(kRedCols * kRedGroups), 0,
+  hipLaunchKernelGGL(grad_reduce_kernel<0>, dim3(kRedColBlocks), dim3(kRedCols * kRedGroups), 0,
                      (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }
 
-int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
-                         int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
+static int reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
+                          int32_t replay_capacity, swarm_ctrl* ctrl, const swarm_peer* peer, void* stream) {
   if (int e = check_td(cfg, hp)) return e;
   if (!lr || !ctrl || replay_capacity < 1) return SWARM_E_BADARG;
   ReduceArgs a = {};
+  if (peer) a.peer = *peer;
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = lr->grad;
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
   a.hp = *hp;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3(kRedColBlocks + 1), dim3(kRedCols * kRedGroups), 0,
-                     (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
+  if (peer)
+    hipLaunchKernelGGL(grad_reduce_kernel<1>, dim3(kRedColBlocks + 1), dim3(kRedCols * kRedGroups), 0,
+                       (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
+  else
+    hipLaunchKernelGGL(grad_reduce_kernel<0>, dim3(kRedColBlocks + 1), dim3(kRedCols * kRedGroups), 0,
+                       (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
+}
+
+int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
+                         int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
+  return reduce_advance(cfg, hp, slabs, lr, replay_capacity, ctrl, nullptr, stream);
+}
+
+int swarm_reduce_advance_peer(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
+                              const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
+                              const swarm_peer* peer, void* stream) {
+  if (int e = check_peer(peer)) return e;
+  if (hp && hp->world_size != peer->world_size) return SWARM_E_BADARG;
+  return reduce_advance(cfg, hp, slabs, lr, replay_capacity, ctrl, peer, stream);
 }
 
 static int launch_adam(const swarm_config* cfg, const swarm_adam_cfg* hp, float* params, float* target, float* m,

@@ -59,10 +59,129 @@ def init_process_group(backend: str, local_rank: Optional[int] = None):
     return dist.group.WORLD
 
 
-def allreduce_grad_(grad: torch.Tensor, world_size: int, group=None) -> torch.Tensor:
+def allreduce_grad_(grad: torch.Tensor, world_size: int, group=None, peer: "PeerExchange" = None) -> torch.Tensor:
     """In-place SUM of the flat gradient over ranks (no-op for one rank without a group).
-    The division by W happens inside the optimizer step (swarm_adam_cfg.world_size)."""
-    if world_size > 1 or group is not None:
+    The division by W happens inside the optimizer step (swarm_adam_cfg.world_size).
+    With a PeerExchange the sum runs as swarm_peer_allreduce (xGMI stores), else over RCCL."""
+    if peer is not None:
+        peer.allreduce_(grad)
+    elif world_size > 1 or group is not None:
         import torch.distributed as dist
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
     return grad
+
+
+class PeerExchange:
+    """One rank's end of the peer all-reduce (include/swarm_hip.h "Peer all-reduce over xGMI").
+
+    The rank allocates one uncached exchange buffer (``swarm_peer_alloc``), exports its HIP IPC
+    handle, gathers every rank's handle over the process group (the group carries only this
+    setup and the bench's barriers; the data path never touches it) and maps the others'
+    buffers.  ``SwarmEngine.train_tick`` then runs ``swarm_reduce_advance_peer``: the slab
+    reduce, the exchange and the rank-ordered sum in ONE launch, graph-capturable, with no RCCL
+    call.  Every rank must issue the same sequence of peer launches (SPMD), as with a collective.
+
+    ``local(W)`` builds W ends in one process over W local buffers: the single-GPU emulation
+    the tests use (W engines on W streams)."""
+
+    def __init__(self, lib, world_size: int, rank: int, own: int, recv: list, device, owned: list,
+                 mapped: list, timeout_us: int = 0):
+        from ._lib import PEER_MAX, PEER_SEQ_WORDS, SwarmPeer, c_void_p
+        self.lib, self.world_size, self.rank, self.device = lib, world_size, rank, torch.device(device)
+        self.own, self._owned, self._mapped = own, owned, mapped
+        self.seq = torch.zeros(PEER_SEQ_WORDS, dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        arr = (c_void_p * PEER_MAX)()
+        for q, p in enumerate(recv):
+            arr[q] = p
+        self.struct = SwarmPeer(world_size, rank, arr, self.seq.data_ptr(), self.err.data_ptr(), int(timeout_us), 0)
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def _alloc(lib) -> int:
+        from ._lib import c_void_p, check
+        import ctypes
+        p = c_void_p()
+        check(lib.swarm_peer_alloc(ctypes.byref(p)), "swarm_peer_alloc")
+        return int(p.value)
+
+    @classmethod
+    def connect(cls, group=None, device=None, timeout_us: int = 0) -> "PeerExchange":
+        """Collective over ``group`` (every rank calls it): allocate, exchange IPC handles, map."""
+        import ctypes
+        import torch.distributed as dist
+        from . import _lib
+        lib = _lib.load()
+        W, r = dist.get_world_size(group), dist.get_rank(group)
+        if W > _lib.PEER_MAX:
+            raise ValueError(f"peer all-reduce supports up to {_lib.PEER_MAX} ranks (one node), got {W}")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        own = cls._alloc(lib)
+        h = (ctypes.c_char * _lib.PEER_HANDLE_BYTES)()
+        _lib.check(lib.swarm_peer_ipc_handle(ctypes.c_void_p(own), h), "swarm_peer_ipc_handle")
+        handles = [None] * W
+        dist.all_gather_object(handles, bytes(h), group=group)
+        recv, mapped = [], []
+        for q, hq in enumerate(handles):
+            if q == r:
+                recv.append(own)
+                continue
+            p = ctypes.c_void_p()
+            buf = (ctypes.c_char * _lib.PEER_HANDLE_BYTES).from_buffer_copy(hq)
+            _lib.check(lib.swarm_peer_ipc_open(buf, ctypes.byref(p)), f"swarm_peer_ipc_open(rank {q})")
+            recv.append(int(p.value))
+            mapped.append(int(p.value))
+        dist.barrier(group)
+        return cls(lib, W, r, own, recv, dev, [own], mapped, timeout_us)
+
+    @classmethod
+    def local(cls, world_size: int, device=None, timeout_us: int = 0) -> list:
+        """W ends in one process (single-GPU emulation of W ranks)."""
+        from . import _lib
+        lib = _lib.load()
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        bufs = [cls._alloc(lib) for _ in range(world_size)]
+        ends = [cls(lib, world_size, r, bufs[r], bufs, dev, [], [], timeout_us) for r in range(world_size)]
+        ends[0]._owned = bufs   # the first end frees them all
+        return ends
+
+    # ------------------------------------------------------------------ use
+    def allreduce_(self, x: torch.Tensor) -> torch.Tensor:
+        """In-place rank-ordered SUM of a flat fp32 device tensor (<= 1,674 elements)."""
+        from ._lib import check, stream_ptr
+        import ctypes
+        assert x.is_contiguous() and x.dtype == torch.float32 and x.device == self.device
+        check(self.lib.swarm_peer_allreduce(ctypes.byref(self.struct), x.data_ptr(), x.numel(), stream_ptr()),
+              "swarm_peer_allreduce")
+        return x
+
+    def errors(self) -> int:
+        """Exchange waits that expired (0 in a correct run); one 4-byte device read."""
+        return int(self.err.item())
+
+    def check(self):
+        n = self.errors()
+        if n:
+            raise RuntimeError(f"peer all-reduce: {n} exchange wait(s) expired (a rank stopped issuing the same "
+                               "sequence of peer launches, or its stores never arrived); the gradients are wrong")
+
+    def selftest(self) -> bool:
+        """Every rank contributes (rank + 1) * (1 + column): the rank-ordered sums are exact
+        small integers.  Returns False on a wrong sum or an expired wait (caller falls back)."""
+        from ._lib import N_PARAMS
+        n = N_PARAMS + 1
+        col = torch.arange(n, dtype=torch.float32, device=self.device)
+        x = (self.rank + 1) * (1 + col)
+        self.allreduce_(x)
+        want = (self.world_size * (self.world_size + 1) / 2) * (1 + col)
+        ok = bool(torch.equal(x, want)) and self.errors() == 0
+        return ok
+
+    def close(self):
+        from ._lib import check
+        import ctypes
+        for p in self._mapped:
+            check(self.lib.swarm_peer_ipc_close(ctypes.c_void_p(p)), "swarm_peer_ipc_close")
+        for p in self._owned:
+            check(self.lib.swarm_peer_free(ctypes.c_void_p(p)), "swarm_peer_free")
+        self._mapped, self._owned = [], []

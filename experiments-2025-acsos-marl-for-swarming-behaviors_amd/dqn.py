@@ -188,6 +188,8 @@ class DQNTrainer:
             average_loss = float(self._acc_loss.item()) / max_steps
             ep_reward = float(self._acc_reward.item())
             eng.check_handoffs()   # an overrun hand-off dropped TD graphs: fail loudly (one 4-byte read)
+            if eng.peer is not None:
+                eng.peer.check()   # an expired peer-exchange wait: the summed gradient is wrong
             self.episode_losses.append(average_loss)
             self.rewards_buffer.append(torch.tensor(ep_reward))
             if (episode + 1) % 10 == 0:

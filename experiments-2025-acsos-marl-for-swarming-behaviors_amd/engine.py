@@ -10,6 +10,10 @@ One fused training tick (the reference's hot loop, src/training/train_gcn_dqn.py
     swarm_reduce_advance  deterministic slab sum, ping-pong copy-back, ctrl advance    (1 launch)
     [all_reduce(grad) over RCCL when world_size > 1]
 
+With a ``PeerExchange`` (dist.py; ``peer=``) the all-reduce is fused into the reduce launch
+(``swarm_reduce_advance_peer``: xGMI stores of the column sums, rank-ordered sum): still two
+launches per tick at any world size, and no collective in the captured graph.
+
 TD graphs drawn from the tick's own replay slot (push before sample, as the reference)
 wait in-kernel for the acting wave of their env (write-through hand-off records in
 ``tick_ws``).  Configurations without a fused-tick kernel (kNN training graph,
@@ -108,7 +112,7 @@ class SwarmEngine:
                  adam_eps: float = 1e-8, max_norm: float = 1.0, update_target_every: int = 200,
                  replay_capacity: int = 1_000_000, env_offset: int = 0, world_size: int = 1,
                  process_group=None, shared_reset: bool = False, random_oa: bool = True, eps: float = 0.05,
-                 device=None, learn: bool = True, net: str = "gcn"):
+                 device=None, learn: bool = True, net: str = "gcn", peer=None):
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.type != "cuda":
@@ -125,6 +129,9 @@ class SwarmEngine:
         self.batch = n_envs if batch is None else batch
         self.world_size = world_size
         self.process_group = process_group
+        if peer is not None and peer.world_size != world_size:
+            raise ValueError(f"peer exchange of {peer.world_size} ranks for world_size {world_size}")
+        self.peer = peer
         self.hp = SwarmAdamCfg(lr, betas[0], betas[1], adam_eps, max_norm, gamma, self.batch,
                                update_target_every, world_size, 0)
         dev = self.device
@@ -261,7 +268,8 @@ class SwarmEngine:
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
     def allreduce_grad(self):
-        allreduce_grad_(self.grad, self.world_size, self.process_group)
+        g = self.grad if self.peer is None else self.grad[:N_PARAMS + 1]   # parameters + loss sum
+        allreduce_grad_(g, self.world_size, self.process_group, self.peer)
 
     def adam(self):
         check(self.lib.swarm_adam_step(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.params), ptr(self.target),
@@ -307,6 +315,13 @@ class SwarmEngine:
                                         ptr(self.tick_ws), ptr(self.samples), stream_ptr()), "swarm_train_tick")
 
     def launch_reduce_advance(self):
+        """Slab reduce + ctrl advance; with a peer exchange, the gradient all-reduce too."""
+        if self.peer is not None:
+            check(self.lib.swarm_reduce_advance_peer(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
+                                                     ctypes_ref(self.learner), self.capacity, ptr(self.ctrl),
+                                                     ctypes_ref(self.peer.struct), stream_ptr()),
+                  "swarm_reduce_advance_peer")
+            return
         check(self.lib.swarm_reduce_advance(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
                                             ctypes_ref(self.learner), self.capacity, ptr(self.ctrl), stream_ptr()),
               "swarm_reduce_advance")
@@ -335,7 +350,8 @@ class SwarmEngine:
             return self.train_tick3(full_out)
         self.launch_tick(full_out)
         self.launch_reduce_advance()
-        self.allreduce_grad()
+        if self.peer is None:
+            self.allreduce_grad()
 
     def train_tick3(self, full_out: bool = False):
         """3-launch training tick: act (+ this tick's TD batch indices), TD, reduce."""
@@ -347,9 +363,9 @@ class SwarmEngine:
         check(self.lib.swarm_td_grad(cfg, hp, ptr(self.w_nxt), ptr(self.target), ctypes_ref(self.replay),
                                      ptr(self.ctrl), ptr(self.samples), None, ptr(self.slabs), stream_ptr()),
               "swarm_td_grad")
-        check(self.lib.swarm_reduce_advance(cfg, hp, ptr(self.slabs), ctypes_ref(self.learner), self.capacity,
-                                            ptr(self.ctrl), stream_ptr()), "swarm_reduce_advance")
-        self.allreduce_grad()
+        self.launch_reduce_advance()
+        if self.peer is None:
+            self.allreduce_grad()
 
     # ------------------------------------------------------------------ hipGraph
     def capture(self, n_ticks: int, fn=None):

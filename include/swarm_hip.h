@@ -7,7 +7,8 @@
  *   - every entry point returns 0 on success, a positive hipError_t, or a
  *     negative SWARM_E_* code; nothing throws across the ABI;
  *   - no allocation, no host synchronisation inside any call: every call can be
- *     captured into a hipGraph.
+ *     captured into a hipGraph (the one exception: the peer exchange's setup calls,
+ *     swarm_peer_alloc / _free / _ipc_*, made once before any tick).
  *
  * Reference interfaces each entry point replaces are cited per function
  * (paths relative to the reference checkout; VMAS 1.4.0 / PyG 2.5.3 are the
@@ -22,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 6
+#define SWARM_ABI_VERSION 7
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
@@ -226,6 +227,53 @@ uint32_t swarm_host_sample_position(uint32_t g, uint32_t n, uint32_t k0, uint32_
  * advance ctrl (tick, replay slot, the next step's Adam scalars). */
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
                          const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
+
+/* ---- Peer all-reduce over xGMI (the one exchange of the data-parallel tick).
+ * The reference has no distributed code; this replaces the RCCL all_reduce(grad) that would
+ * follow swarm_reduce_advance (dist.py allreduce_grad_).  Every rank owns one exchange buffer
+ * (swarm_peer_alloc: uncached device memory, so a peer's xGMI stores are seen by this GPU's
+ * loads without a cache flush) and maps every other rank's buffer through HIP IPC.  A rank
+ * publishes each gradient column as a tagged 8-byte granule {tag, value} with ONE system-scope
+ * store into every rank's buffer (its own included) and polls its own buffer until all W tags
+ * match: the data is its own flag.  The W values of a column are added in rank order, so every
+ * rank computes bitwise the same sum.  Tags come from per-block launch counters (`seq`, device
+ * words zeroed once at setup; every rank must issue the same sequence of peer calls) and the
+ * buffer is double-buffered by their parity, so nothing is ever reset.  Waits are bounded in
+ * time: one that expires adds 1 to *err (the sum is then wrong: check err and fail loudly). */
+#define SWARM_PEER_MAX 8
+#define SWARM_PEER_HANDLE_BYTES 64   /* hipIpcMemHandle_t */
+#define SWARM_PEER_SEQ_WORDS 256     /* launch counters per rank (device uint32, zeroed at setup) */
+typedef struct swarm_peer {
+  int32_t world_size;              /* W, 1..SWARM_PEER_MAX                                     */
+  int32_t rank;                    /* this rank                                                */
+  void* recv[SWARM_PEER_MAX];      /* rank q's exchange buffer as mapped in this process       */
+  uint32_t* seq;                   /* SWARM_PEER_SEQ_WORDS launch counters of this rank        */
+  int32_t* err;                    /* device int32: waits that hit the time bound              */
+  uint32_t timeout_us;             /* bound of one wait (0 = 5 000 000 us: ranks start skewed) */
+  int32_t pad;
+} swarm_peer;
+
+/* Setup (host-synchronous, not for the hot path): bytes of one exchange buffer; allocate one
+ * (zeroed, uncached) / free it; export its IPC handle (SWARM_PEER_HANDLE_BYTES bytes); map a
+ * peer's handle / unmap it. */
+int64_t swarm_peer_buffer_bytes(void);
+int swarm_peer_alloc(void** buf);
+int swarm_peer_free(void* buf);
+int swarm_peer_ipc_handle(void* buf, void* handle);
+int swarm_peer_ipc_open(const void* handle, void** buf);
+int swarm_peer_ipc_close(void* buf);
+
+/* swarm_reduce_advance with the all-reduce fused in: each column block sums its slab columns,
+ * exchanges them with the other ranks and writes lr->grad = the rank-ordered sum over ranks
+ * (ctrl->loss stays this rank's own loss, as with swarm_reduce_advance + RCCL). */
+int swarm_reduce_advance_peer(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
+                              const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
+                              const swarm_peer* peer, void* stream);
+
+/* Standalone in-place SUM all-reduce of x[n] (n <= N_PARAMS + 1) over the ranks of `peer`
+ * (rank-ordered, bitwise identical on every rank); the unfused API path's replacement of
+ * all_reduce(grad), and the setup self-test. */
+int swarm_peer_allreduce(const swarm_peer* peer, float* x, int32_t n, void* stream);
 
 /* Draw the TD batch's replay indices [batch] for the tick ctrl describes
  * (GraphReplayBuffer.sample, train_gcn_dqn.py:40: keyed permutation, distinct ids). */

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _ctypes_structs():
     import swarm_amd._lib as L
     return {"swarm_config": L.SwarmConfig, "swarm_replay": L.SwarmReplay, "swarm_act_out": L.SwarmActOut,
-            "swarm_adam_cfg": L.SwarmAdamCfg, "swarm_learner": L.SwarmLearner}
+            "swarm_adam_cfg": L.SwarmAdamCfg, "swarm_learner": L.SwarmLearner, "swarm_peer": L.SwarmPeer}
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="no C compiler")

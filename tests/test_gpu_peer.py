@@ -1,0 +1,258 @@
+"""GPU tests of the peer all-reduce (include/swarm_hip.h "Peer all-reduce over xGMI"; dist.py
+PeerExchange), the data-parallel tick's one exchange.
+
+On the one-GPU test box W ranks are emulated two ways:
+* in one process: W ``PeerExchange.local`` ends over W local buffers, each rank's launches on
+  its own stream, so the ranks' kernels run side by side and wait on each other's stores;
+* in two processes (``test_two_process_ipc_exchange``): the real setup path, HIP IPC handles
+  exchanged over a gloo group, both processes on the same GPU.
+The reference (single process, CPU) has no distributed code; the contract checked is the
+all-reduce's: every rank ends with the rank-ordered SUM, bitwise identical on every rank, and
+the fused tick with the exchange equals the tick followed by a hand-made sum.
+"""
+import os
+import socket
+import time
+
+import pytest
+import torch
+
+from oracle import swarm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sw():
+    import swarm_amd
+    swarm_amd.load_library()
+    return swarm_amd
+
+
+def _params(golden_weights, seed=1):
+    return torch.tensor(golden_weights["go_to"][seed])
+
+
+@pytest.fixture(scope="module")
+def rank_streams(sw):
+    """Three streams on distinct hardware queues, one per emulated rank.  The ranks' kernels
+    wait on each other's stores, so they must run side by side; HIP maps a process's streams
+    onto GPU_MAX_HW_QUEUES = 4 hardware queues and two pool streams can share one
+    (tools/peer_probe.py: one pair in 16 does).  Candidate sets are checked with a W = 3
+    exchange under a 20 ms bound (an expired wait is counted, never hangs)."""
+    from swarm_amd.dist import PeerExchange
+    probe = PeerExchange.local(3, timeout_us=20000)
+    try:
+        for _ in range(16):
+            ss = [torch.cuda.Stream(priority=-1) for _ in range(3)]
+            x = [torch.ones(16, device="cuda") for _ in range(3)]
+            before = [e.errors() for e in probe]
+            for r, s in enumerate(ss):
+                with torch.cuda.stream(s):
+                    probe[r].allreduce_(x[r])
+            torch.cuda.synchronize()
+            if all(e.errors() == b for e, b in zip(probe, before)) and all(bool((v == 3).all()) for v in x):
+                return ss
+        pytest.fail("no three streams on distinct hardware queues")
+    finally:
+        probe[0].close()
+
+
+def _on_streams(streams, ends, fn):
+    """Run fn(rank) for every rank on its own stream (the ranks' exchanges must overlap)."""
+    cur = torch.cuda.current_stream()
+    streams = streams[:len(ends)]
+    for s in streams:
+        s.wait_stream(cur)
+    for r, s in enumerate(streams):
+        with torch.cuda.stream(s):
+            fn(r)
+    for s in streams:
+        cur.wait_stream(s)
+    torch.cuda.synchronize()
+
+
+# in one process every emulated rank needs a hardware queue of its own (its kernels wait on the
+# others'): the box gives a process GPU_MAX_HW_QUEUES = 4, one of them torch's current stream.
+# More ranks run as processes (test_two_process_ipc_exchange, W = 8).
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_peer_allreduce_sums_in_rank_order(sw, rank_streams, world):
+    from swarm_amd.dist import PeerExchange
+    ends = PeerExchange.local(world)
+    try:
+        g = torch.Generator().manual_seed(world)
+        xs = [torch.randn(O.N_PARAMS + 1, generator=g).cuda() for _ in range(world)]
+        for rep in range(3):   # the double buffer flips parity every launch
+            ys = [x * float(rep + 1) for x in xs]
+            want = ys[0].cpu().clone()
+            for y in ys[1:]:
+                want = want + y.cpu()   # rank order, fp32
+            _on_streams(rank_streams, ends, lambda r: ends[r].allreduce_(ys[r]))
+            for r in range(world):
+                assert torch.equal(ys[r].cpu(), want), (world, rep, r)
+        assert all(e.errors() == 0 for e in ends)
+        if world == 1:
+            assert ends[0].selftest()   # the setup self-test needs no partner at W = 1
+    finally:
+        ends[0].close()
+
+
+def test_peer_wait_expires_and_is_counted(sw):
+    """Only rank 0 of two launches: its waits for rank 1 expire (short bound), are counted, and
+    check() fails loudly."""
+    from swarm_amd.dist import PeerExchange
+    ends = PeerExchange.local(2, timeout_us=2000)
+    try:
+        x = torch.ones(64, device="cuda")
+        ends[0].allreduce_(x)
+        torch.cuda.synchronize()
+        assert ends[0].errors() == 64   # one per column waiting on rank 1
+        with pytest.raises(RuntimeError, match="peer all-reduce"):
+            ends[0].check()
+        assert ends[1].errors() == 0
+    finally:
+        ends[0].close()
+
+
+def test_one_rank_peer_tick_equals_plain_tick(sw, golden_weights):
+    """W = 1: the fused reduce with the exchange is bitwise the plain slab reduce."""
+    from swarm_amd.dist import PeerExchange
+    p = _params(golden_weights)
+    (end,) = PeerExchange.local(1)
+    try:
+        kw = dict(seed=4, params=p, batch=64, replay_capacity=64 * 3, eps=0.2, update_target_every=3)
+        a = sw.SwarmEngine("GoTo", 8, 64, peer=end, **kw)
+        b = sw.SwarmEngine("GoTo", 8, 64, **kw)
+        for e in (a, b):
+            e.reset(0)
+        for _ in range(6):
+            a.train_tick()
+            b.train_tick()
+        torch.cuda.synchronize()
+        assert torch.equal(a.grad, b.grad) and torch.equal(a.params, b.params) and a.read_ctrl() == b.read_ctrl()
+        assert end.errors() == 0
+    finally:
+        end.close()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_two_rank_peer_tick_equals_hand_made_allreduce(sw, rank_streams, golden_weights, fused):
+    """Two world_size=2 engines with a peer exchange (their ticks on two streams) against two
+    engines whose all-reduce is done by hand (g0 + g1, the SUM of dist.allreduce_grad_): the
+    same gradients, weights, moments and control blocks bit for bit, replicas identical; the
+    fused tick and the 3-launch tick."""
+    from swarm_amd.dist import PeerExchange
+    B, N, S, slots = 32, 8, 16, 4
+    p = _params(golden_weights)
+    kw = dict(seed=6, params=p, eps=0.25, update_target_every=3, batch=S, replay_capacity=slots * B, world_size=2)
+    ends = PeerExchange.local(2)
+    try:
+        pa = [sw.SwarmEngine("GoTo", N, B, env_offset=r * B, peer=ends[r], **kw) for r in range(2)]
+        ha = [sw.SwarmEngine("GoTo", N, B, env_offset=r * B, **kw) for r in range(2)]
+        for e in pa + ha:
+            e.reset(0)
+            for _ in range(2):
+                e.act(push=True, full_out=False)
+                e.advance()
+        t0 = time.perf_counter()
+        for t in range(5):
+            _on_streams(rank_streams, pa, lambda r: pa[r].train_tick() if fused else pa[r].train_tick3())
+            for e in ha:   # the ticks without their all-reduce, then the SUM by hand
+                if fused:
+                    e.launch_tick()
+                else:
+                    e.launch_train_act()
+                    e.launch_td()
+                e.launch_reduce_advance()
+            g = ha[0].grad + ha[1].grad
+            for e in ha:
+                e.grad.copy_(g)
+            torch.cuda.synchronize()
+            for r in range(2):
+                assert torch.equal(pa[r].grad[:O.N_PARAMS + 1], ha[r].grad[:O.N_PARAMS + 1]), \
+                    (t, r, [e.errors() for e in ends], time.perf_counter() - t0)
+                assert torch.equal(pa[r].state, ha[r].state) and pa[r].read_ctrl() == ha[r].read_ctrl(), (t, r)
+        for e in pa + ha:
+            e.flush()
+        torch.cuda.synchronize()
+        assert torch.equal(pa[0].params, pa[1].params) and torch.equal(pa[0].adam_v, pa[1].adam_v)
+        assert torch.equal(pa[0].params, ha[0].params) and torch.equal(pa[0].target, ha[0].target)
+        assert all(e.errors() == 0 for e in ends) and pa[0].handoff_errors() == 0
+    finally:
+        ends[0].close()
+
+
+def test_two_rank_peer_ticks_replay_from_captured_graphs(sw, rank_streams, golden_weights):
+    """The bench's launch mode: each rank's episode captured into its own hipGraph (no
+    collective inside), the two graphs replayed side by side on two streams."""
+    from swarm_amd.dist import PeerExchange
+    B, N, S = 64, 8, 64
+    p = _params(golden_weights)
+    kw = dict(seed=2, params=p, eps=0.05, update_target_every=200, batch=S, replay_capacity=3 * B, world_size=2)
+    ends = PeerExchange.local(2)
+    try:
+        ranks = [sw.SwarmEngine("GoTo", N, B, env_offset=r * B, peer=ends[r], **kw) for r in range(2)]
+        for e in ranks:
+            e.reset(0)
+        _on_streams(rank_streams, ranks, lambda r: ranks[r].train_tick())   # eager warm tick
+        graphs = [e.capture(10) for e in ranks]
+        for _ in range(3):
+            _on_streams(rank_streams, ranks, lambda r: graphs[r].replay())
+        for e in ranks:
+            e.flush()
+        torch.cuda.synchronize()
+        assert all(e.errors() == 0 for e in ends)
+        assert torch.equal(ranks[0].params, ranks[1].params) and torch.equal(ranks[0].adam_m, ranks[1].adam_m)
+        c = ranks[0].read_ctrl()
+        assert c["tick"] == 31 and c["adam_step"] >= 29 and torch.isfinite(torch.tensor(c["loss"]))
+    finally:
+        ends[0].close()
+
+
+# ------------------------------------------------------------------ two processes, HIP IPC
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ipc_worker(rank, world, port, weights, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import swarm_amd
+    from swarm_amd.dist import PeerExchange
+    peer = PeerExchange.connect(dist.group.WORLD, timeout_us=500_000)   # a stuck wait fails in 0.5 s
+    ok = peer.selftest()
+    B, N = 64, 8
+    eng = swarm_amd.SwarmEngine("GoTo", N, B, seed=3, params=torch.tensor(weights), eps=0.1, batch=B,
+                                replay_capacity=3 * B, update_target_every=5, env_offset=rank * B,
+                                world_size=world, peer=peer)
+    eng.reset(0)
+    eng.train_tick()
+    g = eng.capture(20)
+    dist.barrier()
+    g.replay()
+    eng.flush()
+    torch.cuda.synchronize()
+    torch.save({"ok": ok, "errors": peer.errors(), "params": eng.params.cpu(), "v": eng.adam_v.cpu(),
+                "ctrl": eng.read_ctrl()}, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    peer.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_two_process_ipc_exchange(sw, golden_weights, tmp_path, world):
+    """W processes sharing the GPU, HIP IPC handles over gloo.  Not W = 8 on one GPU: every
+    rank's 106 reduce blocks of 1,024 threads must be resident at once (they wait on each
+    other), 848 blocks against the 512 that fit on 256 CUs; on a node each rank has its GPU."""
+    import torch.multiprocessing as mp
+    mp.spawn(_ipc_worker, args=(world, _free_port(), golden_weights["go_to"][1], str(tmp_path)), nprocs=world,
+             join=True)
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    assert all(r["ok"] and r["errors"] == 0 for r in res)
+    for r in res[1:]:
+        assert torch.equal(res[0]["params"], r["params"]) and torch.equal(res[0]["v"], r["v"])
+    assert res[0]["ctrl"]["tick"] == 21 and res[0]["ctrl"]["adam_step"] >= 19
