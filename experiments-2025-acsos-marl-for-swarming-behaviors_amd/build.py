@@ -41,10 +41,14 @@ VARIANTS = {"main": (OUT, []), "stamps": (STAMPS_OUT, ["-DSWARM_STAMPS=1"]),
             "hodrop": (HODROP_OUT, ["-DSWARM_HO_FORCE_DROP=1"])}
 
 
-def build(force: bool = False, verbose: bool = True, stamps: bool = False, variant: str = "main") -> str:
+def build(force: bool = False, verbose: bool = True, stamps: bool = False, variant: str = "main",
+          out: str = None, extra: list = None) -> str:
     """stamps=True (or variant="stamps") builds the diagnostic library (in-kernel s_memtime
-    stamps); variant="hodrop" the hand-off overrun test library."""
-    out, extra = VARIANTS["stamps" if stamps else variant]
+    stamps); variant="hodrop" the hand-off overrun test library; out + extra: an A/B build
+    (tools/ab_build.py) with extra compiler flags."""
+    if out is None:
+        out, extra = VARIANTS["stamps" if stamps else variant]
+    extra = list(extra or [])
     if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _deps()):
         return out
     # one hipcc process per translation unit (in parallel), then one link
