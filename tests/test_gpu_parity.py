@@ -508,11 +508,17 @@ def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
                                                         ("GoTo", 5, "gat", 37, 3, "complete"),      # ragged blocks
                                                         ("ObstacleAvoidance", 11, "gcn", 33, 2, "knn"),
                                                         ("Flocking", 8, "gat", 64, 2, "complete"),
-                                                        ("Flocking", 12, "gcn", 48, 3, "knn")])
+                                                        ("Flocking", 12, "gcn", 48, 3, "knn"),
+                                                        # every graph from the tick's own slot, far
+                                                        # more blocks than are resident at once
+                                                        ("GoTo", 8, "gat", 4096, 1, "complete"),
+                                                        ("ObstacleAvoidance", 12, "gat", 2048, 1, "complete")])
 def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, conv, B, slots, graph):
     """swarm_train_tick (acting and TD blocks in one launch, TD graphs of the tick's own slot
-    read through the hand-off records) == the 3-launch tick, bit for bit, every tick.  Small
-    rings make most draws come from the slot being written (slots = 1: all of them)."""
+    read through the hand-off records) == the 3-launch tick, bit for bit, every tick: Q,
+    actions, rewards, gradient, state, replay ring, weights.  Small rings make most draws come
+    from the slot being written (slots = 1: all of them; with 4096 / 2048 envs far more blocks
+    than are resident, so most TD blocks start only after acting blocks have ended)."""
     p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 2)
     kw = dict(seed=9, params=p, batch=B, eps=0.3, update_target_every=3, replay_capacity=slots * B, conv=conv,
               graph=graph, knn_k=5, radius=0.25)
