@@ -127,7 +127,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // fused tick: is this env's transition in the TD batch drawn from this tick's slot?
   // (position of graph id slot * B + env in the keyed permutation < batch)
   bool ho_pub = false;
-  if (MODE == MODE_TICK && HO && d.live) {
+  if (MODE == MODE_TICK && HO && d.live && !SWARM_DIAG_NO_HO) {
     const uint32_t cap = (uint32_t)A.replay.capacity;
     const uint32_t filled = cc.filled_slots;
     const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)B;
@@ -180,6 +180,9 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   __syncthreads();   // weight image complete
   const float* P = Pw;
   SWARM_STAMP(1);
+#if SWARM_DIAG_ACT   // diagnostic A/B builds only: acting waves stop after the optimizer step
+  if (MODE == MODE_TICK && HO && (SWARM_DIAG_ACT == 2 || (w & 1))) return;
+#endif
 
   const int n_ticks = (MODE == MODE_ROLLOUT) ? A.n_ticks : 1;
   float rew_sum[CT], hits_sum = 0.0f;

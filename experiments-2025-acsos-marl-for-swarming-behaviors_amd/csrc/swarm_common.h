@@ -12,6 +12,14 @@
 
 #include "../../include/swarm_hip.h"
 
+// diagnostic A/B knobs (tools/ab_build.py only; 0 in every shipped library)
+#ifndef SWARM_DIAG_NO_HO
+#define SWARM_DIAG_NO_HO 0   // fused tick: no hand-offs (TD reads the ring slot as written so far)
+#endif
+#ifndef SWARM_DIAG_ACT
+#define SWARM_DIAG_ACT 0     // fused tick: 1 = odd acting waves, 2 = every acting wave stops after Adam
+#endif
+
 namespace swarm {
 
 // ---------------------------------------------------------------- constants

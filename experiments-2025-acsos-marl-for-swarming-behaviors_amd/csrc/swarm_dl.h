@@ -147,6 +147,111 @@ __device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& 
   return topk_smallest_mask<GS>(d, N, k, q);
 }
 
+// t-th (1-based) lowest / highest set bit of a lane mask
+__device__ inline int bit_sel_low(uint32_t m, int t) {
+  for (int i = 1; i < t; ++i) m &= m - 1u;
+  return __ffs(m) - 1;
+}
+__device__ inline int bit_sel_high(uint32_t m, int t) {
+  for (int i = 1; i < t; ++i) m &= ~(1u << (31 - __clz(m)));
+  return 31 - __clz(m);
+}
+
+// The boundary-tie rows of knn_masks_wave, G lanes per row (one element per lane, G >= the
+// graph's node count): libstdc++'s introselect (swarm_knn.h kv_nth_element) restated on the
+// group's lanes.  Median-of-3 is a swap of two lanes; the unguarded partition is one step:
+// with L_1 < L_2 < ... the left stoppers (!(v < pivot), from first + 1) and R_1 > R_2 > ...
+// the right stoppers (!(pivot < v), down to the pivot itself), the scans swap (L_t, R_t)
+// exactly while L_t < R_t (t <= T) and return cut = L_1 (T = 0) or min(L_{T+1}, R_T) — every
+// scan between two swaps runs over unswapped elements, and each swapped element is a stopper
+// for the other scan.  The final insertion sort of <= 3 elements is a stable rank sort.  The
+// heap_select branch (depth limit) runs serially in LDS as before.  Checked against
+// torch.topk on 60,000 tie-heavy rows (n 4..16) before it went in; the GPU tests compare the
+// sets with torch.topk (oracle knn_sets) and the recorded reference actions.
+// tb: ballot with bit n * lpn set for every tie row n; q: GS KV entries of LDS per slot.
+template <int NS, int GS>
+__device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
+                                         const float* __restrict__ dn, KV* q) {
+  constexpr int G = GS <= 8 ? 8 : 16;   // lanes per row
+  constexpr int NG = 64 / G;
+  const int g = lane / G, e = lane % G, gb = lane - e;
+  auto gballot = [&](bool x) -> uint32_t { return (uint32_t)((__ballot(x) >> gb) & ((1ull << G) - 1ull)); };
+  while (tb) {
+    unsigned long long t = tb;
+    for (int i = 0; i < g && t; ++i) t &= t - 1ull;   // this group's row: the g-th remaining
+    for (int i = 0; i < NG && tb; ++i) tb &= tb - 1ull;
+    if (t == 0ull) continue;
+    const int n = (__ffsll((long long)t) - 1) / lpn;
+    float v = e < N ? dn[n * GS + e] : 0.0f;
+    int id = e;
+    const int nth = k - 1;
+    int first = 0, last = N;
+    int depth = 2 * floor_log2(N);
+    bool heap = false;
+    while (last - first > 3) {   // group-uniform control flow
+      if (depth == 0) { heap = true; break; }
+      --depth;
+      const int mid = first + (last - first) / 2;
+      const float vx = __shfl(v, gb + first + 1), vy = __shfl(v, gb + mid), vz = __shfl(v, gb + last - 1);
+      int pick;   // kv_move_median_to_first(first, first + 1, mid, last - 1)
+      if (vx < vy) pick = (vy < vz) ? mid : ((vx < vz) ? last - 1 : first + 1);
+      else if (vx < vz) pick = first + 1;
+      else pick = (vy < vz) ? last - 1 : mid;
+      int src = e == first ? pick : (e == pick ? first : e);
+      v = __shfl(v, gb + src);
+      id = __shfl(id, gb + src);
+      const float pv = __shfl(v, gb + first);
+      const uint32_t lm = gballot(e > first && e < last && !(v < pv));
+      const uint32_t rm = gballot(e >= first && e < last && !(pv < v));
+      const bool is_l = (lm >> e) & 1u, is_r = (rm >> e) & 1u;
+      const int tl = __popc(lm & ((1u << e) - 1u)) + 1;   // rank among the left stoppers
+      const int above = __popc(rm >> (e + 1));             // right stoppers after e
+      const int T = __popc(gballot(is_l && above >= tl));
+      src = e;
+      if (is_l && tl <= T) src = bit_sel_high(rm, tl);
+      if (is_r && above + 1 <= T) src = bit_sel_low(lm, above + 1);
+      v = __shfl(v, gb + src);
+      id = __shfl(id, gb + src);
+      int cut = __ffs(lm) - 1;
+      if (T > 0) {
+        cut = bit_sel_high(rm, T);
+        if (__popc(lm) > T) cut = min(cut, bit_sel_low(lm, T + 1));
+      }
+      if (cut <= nth) first = cut;
+      else last = cut;
+    }
+    if (heap) {   // depth limit: heap_select + swap, serially (kv_nth_element)
+      KV* a = q + n * GS;
+      if (e < N) a[e] = KV{v, id};
+      wave_lds_sync();
+      if (e == 0) {
+        kv_heap_select(a, first, nth + 1, last);
+        kv_swap(a, first, nth);
+      }
+      wave_lds_sync();
+      if (e < N) { v = a[e].v; id = a[e].i; }
+    } else {      // kv_insertion_sort of [first, last), <= 3 elements: stable rank sort
+      const bool in = e >= first && e < last;
+      int rank = 0;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int pj = first + j;
+        const float vj = __shfl(v, gb + min(pj, G - 1));
+        if (pj < last) rank += (vj < v || (vj == v && pj < e)) ? 1 : 0;
+      }
+      const uint32_t r0 = gballot(in && rank == 0), r1 = gballot(in && rank == 1), r2 = gballot(in && rank == 2);
+      const uint32_t rm = e - first == 0 ? r0 : (e - first == 1 ? r1 : r2);
+      const int src = in ? __ffs(rm) - 1 : e;
+      v = __shfl(v, gb + src);
+      id = __shfl(id, gb + src);
+    }
+    uint32_t mm = e < k ? (1u << id) : 0u;
+#pragma unroll
+    for (int s = G / 2; s >= 1; s >>= 1) mm |= (uint32_t)__shfl_xor((int)mm, s);
+    if (e == 0) sm.knn[n] = mm;
+  }
+}
+
 // kNN rows of every slot of the wave at once (NS <= 16): lane l serves slot n = l / LPN and
 // the candidates j = l % LPN + LPN i of n's graph.  Each pair distance is computed once
 // (the same fp32 expression as knn_mask_node), the graph's distance rows meet in LDS
@@ -183,9 +288,12 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
     const uint64_t b = __ballot(nvalid && j < N && lt < k);
     mask |= (uint32_t)((b >> (n * LPN)) & ((1ull << LPN) - 1ull)) << (LPN * i);
   }
-  if (r == 0) {
-    if (nvalid && __popc(mask) != k) mask = topk_tie_mask<GS>(row, N, k, q + n * GS);
-    sm.knn[n] = nvalid ? mask : 0u;
+  const bool tie = r == 0 && nvalid && __popc(mask) != k;
+  if (r == 0) sm.knn[n] = nvalid ? mask : 0u;
+  const unsigned long long tb = __ballot(tie);
+  if (tb) {   // boundary ties: the introselect restatement, G lanes per row
+    wave_lds_sync();
+    knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
   }
 }
 

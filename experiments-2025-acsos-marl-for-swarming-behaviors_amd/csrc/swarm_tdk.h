@@ -226,7 +226,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   bool wait = false;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
-    ho[ct] = FUSED && live[ct] && n_graphs >= (uint32_t)S && gid[ct] / (uint32_t)B == cc.write_slot;
+    ho[ct] = FUSED && !SWARM_DIAG_NO_HO && live[ct] && n_graphs >= (uint32_t)S && gid[ct] / (uint32_t)B == cc.write_slot;
     wait = wait || ho[ct];
   }
   // replay rows written by earlier ticks: loads issued now (fused: every lane but the hand-off ones)

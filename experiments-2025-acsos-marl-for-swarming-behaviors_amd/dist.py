@@ -121,18 +121,27 @@ class PeerExchange:
         _lib.check(lib.swarm_peer_ipc_handle(ctypes.c_void_p(own), h), "swarm_peer_ipc_handle")
         handles = [None] * W
         dist.all_gather_object(handles, bytes(h), group=group)
-        recv, mapped = [], []
+        recv, mapped, err = [], [], None
         for q, hq in enumerate(handles):
             if q == r:
                 recv.append(own)
                 continue
             p = ctypes.c_void_p()
             buf = (ctypes.c_char * _lib.PEER_HANDLE_BYTES).from_buffer_copy(hq)
-            _lib.check(lib.swarm_peer_ipc_open(buf, ctypes.byref(p)), f"swarm_peer_ipc_open(rank {q})")
+            try:
+                _lib.check(lib.swarm_peer_ipc_open(buf, ctypes.byref(p)), f"swarm_peer_ipc_open(rank {q})")
+            except RuntimeError as e:   # keep going: every rank must still reach the barrier below
+                err = err or e
+                recv.append(None)
+                continue
             recv.append(int(p.value))
             mapped.append(int(p.value))
         dist.barrier(group)
-        return cls(lib, W, r, own, recv, dev, [own], mapped, timeout_us)
+        end = cls(lib, W, r, own, [x or 0 for x in recv], dev, [own], mapped, timeout_us)
+        if err is not None:   # the caller falls back; the other ranks' self-tests expire on this one
+            end.close()
+            raise err
+        return end
 
     @classmethod
     def local(cls, world_size: int, device=None, timeout_us: int = 0) -> list:

@@ -143,3 +143,89 @@ def topk_smallest_set(values, k):
     q = [(float(values[j]), j) for j in range(n)]
     nth_element(q, k - 1)
     return sorted(j for _, j in q[:k])
+
+
+# ---------------------------------------------------------------------------
+# The same selection as the device computes it: one element per lane of a G-lane group
+# (csrc/swarm_dl.h knn_tie_rows_wave).  Each partition round of the introselect loop is one
+# parallel step over the left stoppers L_1 < L_2 < ... (!(v < pivot) in [first+1, last)) and the
+# right stoppers R_1 > R_2 > ... (!(pivot < v) in [first, last)): the scans swap (L_t, R_t)
+# exactly for t <= T, T = #{t : L_t < R_t}, and return L_1 (T = 0) or min(L_{T+1}, R_T).
+# Readable restatement for the tests; pinned to torch.topk by tests/test_cpu_host.py.
+
+def _sel_low(m, t):
+    for _ in range(t - 1):
+        m &= m - 1
+    return (m & -m).bit_length() - 1
+
+
+def _sel_high(m, t):
+    for _ in range(t - 1):
+        m &= ~(1 << (m.bit_length() - 1))
+    return m.bit_length() - 1
+
+
+def nth_element_lanes(a, nth):
+    """nth_element on a list of (value, index) pairs, lane-parallel form (see above)."""
+    n = len(a)
+    first, last = 0, n
+    if first == last or nth == last:
+        return
+    depth = 2 * (n.bit_length() - 1)
+    while last - first > 3:
+        if depth == 0:   # depth limit: the serial heap_select (as kv_nth_element)
+            _heap_select(a, first, nth + 1, last)
+            a[first], a[nth] = a[nth], a[first]
+            return
+        depth -= 1
+        mid = first + (last - first) // 2
+        x, y, z = first + 1, mid, last - 1
+        if _lt(a[x], a[y]):
+            pick = y if _lt(a[y], a[z]) else (z if _lt(a[x], a[z]) else x)
+        elif _lt(a[x], a[z]):
+            pick = x
+        else:
+            pick = z if _lt(a[y], a[z]) else y
+        a[first], a[pick] = a[pick], a[first]
+        pv = a[first]
+        lm = sum(1 << e for e in range(first + 1, last) if not _lt(a[e], pv))
+        rm = sum(1 << e for e in range(first, last) if not _lt(pv, a[e]))
+        T = sum(1 for e in range(n) if lm >> e & 1 and bin(rm >> (e + 1)).count("1") >= bin(lm & ((1 << e) - 1)).count("1") + 1)
+        src = list(range(n))
+        for e in range(n):
+            if lm >> e & 1:
+                t = bin(lm & ((1 << e) - 1)).count("1") + 1
+                if t <= T:
+                    src[e] = _sel_high(rm, t)
+            if rm >> e & 1:
+                s = bin(rm >> (e + 1)).count("1") + 1
+                if s <= T:
+                    src[e] = _sel_low(lm, s)
+        a[:] = [a[s] for s in src]
+        cut = _sel_low(lm, 1)
+        if T > 0:
+            cut = _sel_high(rm, T)
+            if bin(lm).count("1") > T:
+                cut = min(cut, _sel_low(lm, T + 1))
+        if cut <= nth:
+            first = cut
+        else:
+            last = cut
+    # insertion sort of <= 3 elements == stable sort by value
+    a[first:last] = sorted(a[first:last], key=lambda kv: kv[0])
+
+
+def topk_smallest_set_lanes(values, k):
+    """topk_smallest_set through the lane-parallel restatement."""
+    n = len(values)
+    if k > n:
+        raise RuntimeError("selected index k out of range")
+    q = [(float(values[j]), j) for j in range(n)]
+    nth_element_lanes(q, k - 1)
+    return sorted(j for _, j in q[:k])
+
+
+# A boundary-tie row (n = 15, k = 9: two 9s straddle the k-th place) whose introselect runs out
+# of depth and ends in heap_select (found by search; exercised on the GPU by
+# tests/test_gpu_parity.py test_acting_knn_ties_match_torch_topk)
+HEAP_PATH_ROW = ([1, 12, 4, 11, 5, 13, 10, 14, 9, 8, 2, 3, 0, 6, 9], 9)

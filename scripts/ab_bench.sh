@@ -12,7 +12,7 @@ for rep in $(seq $REPS); do
     SWARM_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu-baseline $BENCH_ARGS > gpurun_out/ab_$v.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; tail -5 gpurun_out/ab_$v.log; exit $rc; fi
-    python -c "import json,sys; d=json.loads(open('gpurun_out/ab_$v.log').read().strip().splitlines()[-1]); print(json.dumps({'variant':'$v','rep':$rep,'us_per_tick':d['us_per_tick'],'tick_us':d['tick_us'],'kernel_us':(d['roofline'] or {}).get('kernel_us')}))" >> gpurun_out/ab.jsonl
+    python -c "import json,sys; d=json.loads(open('gpurun_out/ab_$v.log').read().strip().splitlines()[-1]); print(json.dumps({'variant':'$v','rep':$rep,'value':d['value'],'ms_per_step':d['ms_per_step'],'us_per_tick':d.get('us_per_tick'),'tick_us':d.get('tick_us'),'kernel_us':(d['roofline'] or {}).get('kernel_us')}))" >> gpurun_out/ab.jsonl
   done
 done
 cat gpurun_out/ab.jsonl

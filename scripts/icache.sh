@@ -18,7 +18,7 @@ vals=collections.defaultdict(list)
 for f in glob.glob('gpurun_out/icache/p*/run_counter_collection.csv'):
     for r in csv.DictReader(open(f)):
         k=r['Kernel_Name']
-        key='act' if 'act_kernel' in k else 'td' if 'td_kernel' in k else 'red' if 'reduce' in k else None
+        key='tick' if 'tick_kernel' in k else 'act' if 'act_kernel' in k else 'td' if 'td_kernel' in k else 'red' if 'reduce' in k else None
         if key: vals[(key,r['Counter_Name'])].append(float(r['Counter_Value']))
 for (k,c),v in sorted(vals.items()): print(k,c,statistics.median(v))
 PY

@@ -41,6 +41,33 @@ def test_topk_emulation_matches_torch_fixture():
         assert knn_select.topk_smallest_set(row[:n], int(k)) == sorted(np.where(s)[0].tolist())
 
 
+def test_lane_parallel_topk_restatement_matches_torch():
+    """The lane-parallel partition step of the device's tie path (csrc/swarm_dl.h
+    knn_tie_rows_wave, restated as knn_select.nth_element_lanes) selects torch.topk's set: the
+    committed tie fixture, 3,000 fresh tie-heavy rows against torch.topk itself, and a row that
+    ends in heap_select (depth limit)."""
+    import random
+    import torch
+    z = np.load(os.path.join(ROOT, "tests", "golden", "topk_ties.npz"))
+    for row, (n, k), s in zip(z["dist"], z["nk"], z["sets"]):
+        assert knn_select.topk_smallest_set_lanes(row[:n], int(k)) == sorted(np.where(s)[0].tolist())
+    rng = random.Random(7)
+    for trial in range(3000):
+        n = rng.randint(4, 16)
+        k = rng.randint(1, n)
+        if trial % 2:
+            vals = [float(rng.randint(0, 3)) for _ in range(n)]
+        else:
+            vals = [rng.choice([0.15, 0.3, 0.2121, 0.3354]) for _ in range(n)]
+        d = torch.tensor(vals, dtype=torch.float32)
+        want = sorted(torch.topk(d, k, largest=False).indices.tolist())
+        assert knn_select.topk_smallest_set_lanes(d.tolist(), k) == want, (vals, k)
+    vals, k = knn_select.HEAP_PATH_ROW
+    d = torch.tensor(vals, dtype=torch.float32)
+    want = sorted(torch.topk(d, k, largest=False).indices.tolist())
+    assert knn_select.topk_smallest_set_lanes(vals, k) == knn_select.topk_smallest_set(vals, k) == want
+
+
 def test_host_topk_matches_torch_fixture():
     """The C++ selection the kernels run (swarm_knn.h), compiled for the host."""
     L, lib = _host_lib()

@@ -161,6 +161,35 @@ def test_knn_graph_bit_exact(sw, N, k):
         assert torch.equal(mult[: B * N * N].view(B, N, N).cpu().float(), O.multiplicity_complete(B, N))
 
 
+@pytest.mark.parametrize("N,k", [(5, 3), (8, 5), (8, 2), (12, 5), (12, 10), (16, 7), (16, 15), (15, 9)])
+def test_acting_knn_ties_match_torch_topk(sw, golden_weights, N, k):
+    """The acting path's kNN build (knn_masks_wave, boundary ties through the G-lane
+    introselect restatement knn_tie_rows_wave) on tie-heavy formations: lattice positions in
+    multiples of 1/8 (exact, mostly equal distances; duplicated agents) give edge multiplicities
+    equal to torch.topk's sets (oracle knn_sets) bit for bit.  N = 15, k = 9 carries
+    knn_select.HEAP_PATH_ROW in env 0 (the depth-limit heap_select branch)."""
+    from oracle import knn_select
+    B = 256
+    g = torch.Generator().manual_seed(N * 100 + k)
+    pos = torch.randint(-3, 4, (B, N, 2), generator=g).float() * 0.125
+    if (N, k) == (15, 9):
+        vals, _ = knn_select.HEAP_PATH_ROW
+        pos[0, :, 0] = torch.tensor(vals, dtype=torch.float32) * 0.125
+        pos[0, :, 1] = 0.0
+    vel = torch.zeros(B, N, 2)
+    p = _params(golden_weights, "go_to", 1)
+    eng = sw.SwarmEngine("GoTo", N, B, seed=2, params=p, graph="knn", knn_k=k, eps=0.0, replay_capacity=B)
+    eng.set_state(pos, vel)
+    mult = torch.zeros(B * N * N, dtype=torch.uint8, device="cuda")
+    eng.out.mult = mult.data_ptr()
+    eng.act(push=False, full_out=True)
+    torch.cuda.synchronize()
+    assert torch.equal(mult.view(B, N, N).cpu().float(), O.multiplicity_knn(O.knn_sets(pos, k)))
+    if k < N:   # the tie path really ran: rows whose k-th and (k+1)-th distances are equal
+        d = torch.linalg.norm(pos[:, None, :, :] - pos[:, :, None, :], dim=-1).sort(dim=-1).values
+        assert int((d[..., k - 1] == d[..., k]).sum()) > B // 8
+
+
 @pytest.mark.parametrize("N,radius", [(5, 0.15), (8, 0.15), (8, 0.3), (12, 0.2), (16, 0.25), (29, 0.2)])
 def test_radius_graph_bit_exact(sw, N, radius):
     """Radius-neighbour graph (north_star; not in the reference, parity unpinned): the
