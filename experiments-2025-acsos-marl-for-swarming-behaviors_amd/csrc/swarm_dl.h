@@ -390,12 +390,19 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
       float e[GS];
       int m[GS];
       in_mults<NS, GS>(n, N, graph, sm, dense, d.gid, m);
-      float emax = -INFINITY;
+      // the max over present edges as a tree (max is exact: the serial order's value, three
+      // dependent steps instead of GS)
+      float mx[GS];
 #pragma unroll
       for (int j = 0; j < GS; ++j) {
         e[j] = leaky(sm.ssrc[base + j] + F.sdst[ct]);
-        emax = m[j] > 0 ? fmaxf(emax, e[j]) : emax;
+        mx[j] = m[j] > 0 ? e[j] : -INFINITY;
       }
+#pragma unroll
+      for (int w = GS / 2; w >= 1; w >>= 1)
+#pragma unroll
+        for (int j = 0; j < w; ++j) mx[j] = fmaxf(mx[j], mx[j + w]);
+      const float emax = mx[0];
       float den = 0.0f;
 #pragma unroll
       for (int j = 0; j < GS; ++j) {

@@ -25,8 +25,12 @@ union TickSmem {
   TdSmem<NST> t;
 };
 
+// Occupancy target: with N <= 8 (GS = 8) the grid is 2 blocks per CU at C2 (512 blocks, 256
+// CUs), so 2 waves per SIMD is all it needs, and at that target the compiler keeps the MFMA
+// accumulators in ArchVGPRs (no AGPR copies): 15.22 -> 15.07 us per tick (profiles/r02_ab_wpe.jsonl).
+// N > 8 (one graph per TD wave) keeps 3: C3's 768 blocks must all be resident.
 template <int NSA, int NST, int GS, int SCEN, int SPEC>
-__global__ __launch_bounds__(256) void tick_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2 : 3, GS == 8 ? 2 : 3))) void tick_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
                                                    const float* grad, const float* w_cur, const float* m_cur,
                                                    const float* v_cur, int B, int N, int n_act, ActArgs A,
                                                    TdArgs T, TdFused X) {
