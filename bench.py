@@ -329,7 +329,9 @@ def main():
             kname, pmcf = "td_kernel (swarm_td_grad)", "r01_pmc_td.json"
         ach = flops / t_k / 1e12
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", pmcf)
+        pmc = os.path.join(ROOT, "profiles", pmcf.replace("r01_", "r02_"))   # this round's passes if present
+        if not os.path.exists(pmc):
+            pmc = os.path.join(ROOT, "profiles", pmcf)
         if os.path.exists(pmc) and headline:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         roof = {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
