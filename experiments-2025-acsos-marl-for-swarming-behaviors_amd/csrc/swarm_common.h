@@ -170,6 +170,25 @@ __host__ __device__ inline uint32_t sample_position(uint32_t g, const SampleKey&
   return x;
 }
 
+// ---------------------------------------------------------------- gradient slabs
+// Each TD block writes its partial gradient (N_PARAMS + 1 columns, the last the loss sum) as a
+// slab; the reduce launch sums column block j (16 columns) over all slabs in block order.
+// Layout: column-block major, [kSlabColBlocks][n_slabs][16], so one reduce block reads one
+// contiguous n_slabs x 64 B run (whole 128-B lines, each fetched by one block) instead of a
+// 64-B piece of every 6.7-KB slab row.  SWARM_SLAB_T = 0: the row-major [n_slabs][N_PARAMS + 1].
+#ifndef SWARM_SLAB_T
+#define SWARM_SLAB_T 1
+#endif
+constexpr int kSlabCols = 16;
+constexpr int kSlabColBlocks = (N_PARAMS + 1 + kSlabCols - 1) / kSlabCols;
+__host__ __device__ constexpr size_t slab_floats_per_block() {
+  return SWARM_SLAB_T ? (size_t)kSlabColBlocks * kSlabCols : (size_t)(N_PARAMS + 1);
+}
+__host__ __device__ inline size_t slab_index(int q, int b, int n_slabs) {
+  return SWARM_SLAB_T ? ((size_t)(q / kSlabCols) * n_slabs + b) * kSlabCols + (q % kSlabCols)
+                      : (size_t)b * (N_PARAMS + 1) + q;
+}
+
 // ---------------------------------------------------------------- fused-tick hand-off
 // The fused training tick (swarm_tick.hip) runs the acting blocks beside the TD blocks.
 // A TD graph drawn from THIS tick's replay slot is the transition an acting wave is still

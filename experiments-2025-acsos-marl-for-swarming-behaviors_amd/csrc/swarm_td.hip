@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   float v0[kChunk];
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
-    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[(size_t)(b0 + j) * (N_PARAMS + 1) + col] : 0.0f;
+    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[slab_index(col, b0 + j, n_slabs)] : 0.0f;
   float s = v0[0];
 #pragma unroll
   for (int j = 1; j < kChunk; ++j) s = s + v0[j];
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     for (int b = b0 + kChunk; b < b1; b += kChunk) {
       float v[kChunk];
 #pragma unroll
-      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? slabs[(size_t)(b + j) * (N_PARAMS + 1) + col] : 0.0f;
+      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? slabs[slab_index(col, b + j, n_slabs)] : 0.0f;
 #pragma unroll
       for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }
@@ -287,7 +287,7 @@ extern "C" {
 
 int64_t swarm_td_workspace_floats(const swarm_config* cfg, int32_t batch) {
   if (!cfg || cfg->n_agents < 1 || cfg->n_agents > 32 || batch < 1) return SWARM_E_BADARG;
-  return (int64_t)td_max_blocks(cfg, batch) * (N_PARAMS + 1);
+  return (int64_t)(td_max_blocks(cfg, batch) * slab_floats_per_block());
 }
 
 int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* params, const float* target,
@@ -305,6 +305,7 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.gamma = hp->gamma;
   a.grad_scale = (float)(2.0 / ((double)hp->batch * (double)cfg->n_agents));
   const int nb = td_blocks(cfg, hp->batch);
+  a.n_slabs = nb;
   hipStream_t st = (hipStream_t)stream;
   const int spec = spec_of(a.graph, a.conv);   // training graphs are complete: GAT and GCN specialised
 #define SWARM_TD_LAUNCH1(NS, GS, NT, SP)                                                                       \

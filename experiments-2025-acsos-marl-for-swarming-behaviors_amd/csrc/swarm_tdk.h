@@ -69,6 +69,7 @@ struct TdArgs {
   float* slabs;
   float gamma;
   float grad_scale;   // fp32(2 / M_local)
+  int n_slabs;        // TD blocks of the launch (slab layout, swarm_common.h slab_index)
 };
 
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
@@ -176,7 +177,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.target_view(wi);
   const int lane = d.lane, c = d.c, p = d.p;
-  float* gslab = A.slabs + (size_t)vb * (N_PARAMS + 1);
+  // this block's slab column q (swarm_common.h slab_index: column-block major)
+  auto gslab = [&](int q) { return A.slabs + slab_index(q, vb, A.n_slabs); };
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
@@ -248,7 +250,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
   if (n_graphs < (uint32_t)S) {
-    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) slab_st(gslab + (q), 0.0f);
+    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) slab_st(gslab(q), 0.0f);
     return;
   }
   if (A.sample_out && online && p == 0) {
@@ -551,7 +553,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       if (job == 0) {
         const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) slab_st(gslab + (OFF_W1 + acc_row(r, h) * kHidden + col), dW1[r]);
+        for (int r = 0; r < 16; ++r) slab_st(gslab(OFF_W1 + acc_row(r, h) * kHidden + col), dW1[r]);
       } else if (job == 1) {
         f32x16 dW2 = {};
 #pragma unroll
@@ -563,7 +565,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int a = acc_row(r, h);
-          if (a < kActions) slab_st(gslab + (OFF_W2 + a * kHidden + col), dW2[r]);
+          if (a < kActions) slab_st(gslab(OFF_W2 + a * kHidden + col), dW2[r]);
         }
         if (lane < kActions || lane == 63) {   // every read issued before the ordered sum
           float v[kTdRows];
@@ -572,7 +574,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
           float acc = v[0];
 #pragma unroll
           for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-          slab_st(gslab + (lane == 63 ? N_PARAMS : OFF_B2 + lane), acc);
+          slab_st(gslab(lane == 63 ? N_PARAMS : OFF_B2 + lane), acc);
         }
       } else {
         if (lane < kHidden) {
@@ -582,7 +584,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
           float acc = v[0];
 #pragma unroll
           for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-          slab_st(gslab + (OFF_B1 + lane), acc);
+          slab_st(gslab(OFF_B1 + lane), acc);
         }
       }
     }
@@ -605,7 +607,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         }
         if (c < kFeat) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) slab_st(gslab + (OFF_W + (16 * t + 4 * p + r) * kFeat + c), acc[r]);
+          for (int r = 0; r < 4; ++r) slab_st(gslab(OFF_W + (16 * t + 4 * p + r) * kFeat + c), acc[r]);
         }
       } else if (job == 2) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
         const float* da = h == 0 ? TB.das : TB.dad;
@@ -615,7 +617,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        slab_st(gslab + ((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col), acc);
+        slab_st(gslab((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col), acc);
       } else if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
@@ -623,7 +625,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        slab_st(gslab + (OFF_BIAS + lane), acc);
+        slab_st(gslab(OFF_BIAS + lane), acc);
       }
     }
   }

@@ -107,6 +107,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   const int n_act = (B + kActWPB - 1) / kActWPB;
   const int gs = N <= 8 ? 8 : 16;
   const int n_td = (hp->batch + (kTdRows / gs) - 1) / (kTdRows / gs);
+  t.n_slabs = n_td;
   const dim3 grid(n_act + n_td), block(256);
   hipStream_t st = (hipStream_t)stream;
   const float *g = lr->grad, *w = lr->w_cur, *m = lr->m_cur, *v = lr->v_cur;
