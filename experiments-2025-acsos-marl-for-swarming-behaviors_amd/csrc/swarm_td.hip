@@ -48,6 +48,8 @@ struct ReduceArgs {
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
 #ifndef SWARM_RED_COLS
 #define SWARM_RED_COLS 16
+#endif
+#ifndef SWARM_RED_GROUPS
 #define SWARM_RED_GROUPS 64
 #endif
 constexpr int kRedCols = SWARM_RED_COLS;
