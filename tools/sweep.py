@@ -52,5 +52,6 @@ with open(OUT, "w") as f:
         f.write(json.dumps(line) + "\n")
         f.flush()
         r = line.get("roofline") or {}
-        print(f"{name:40s} {line['value'] / 1e6:9.1f} M agent-steps/s  {line['ms_per_step'] * 1e3:7.2f} us/step  "
+        tick_us = line.get("us_per_tick") or line["ms_per_step"] * 10   # acting: 100-tick episodes
+        print(f"{name:40s} {line['value'] / 1e6:9.1f} M agent-steps/s  {tick_us:7.2f} us/tick  "
               f"frac={r.get('frac', float('nan')):.4f}", flush=True)
