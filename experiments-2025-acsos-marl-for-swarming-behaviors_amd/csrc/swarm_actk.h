@@ -308,6 +308,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       }
     }
     if (it == 0) SWARM_STAMP(3);
+    if (MODE == MODE_TICK && HO && ho_r) SWARM_RTSTAMP(29);   // s' published (stamps build only)
     wave_lds_sync();
     float rf = 0.0f;   // flocking: the collective reward
     if (SCEN == SWARM_FLOCKING) {

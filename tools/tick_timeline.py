@@ -53,15 +53,17 @@ def main():
         ae = us(act[..., 31][act[..., 31] > 0])
         te = us(td[..., 9][td[..., 9] > 0])
         ts = us(td[..., 8][td[..., 8] > 0])
-        pub = us(act[..., 25][act[..., 25] > 0])
+        pub = us(act[..., 29][act[..., 29] > 0])   # hand-off waves: s' published
         ho = td[..., 10]
         blocks_waiting = np.where((ho > 0).any(axis=1))[0]
         print(f"tick {rep}: act waves end median {np.median(ae):.2f} max {ae.max():.2f} us; "
               f"TD waves start median {np.median(ts):.2f}, end median {np.median(te):.2f} max {te.max():.2f} us")
-        print(f"  {len(pub)} acting waves published (at {np.sort(pub).round(2).tolist()[:12]} us)")
+        print(f"  {len(pub)} acting waves published s' (at {np.sort(pub).round(2).tolist()[:12]} us)")
         for b in blocks_waiting[:12]:
-            hw = us(ho[b][ho[b] > 0])
-            print(f"  TD block {b}: hand-off at {hw.round(2).tolist()} us, block end {us(td[b, :, 9].max()):.2f} us")
+            on = us(ho[b, :2][ho[b, :2] > 0])
+            tg = us(ho[b, 2:][ho[b, 2:] > 0])
+            print(f"  TD block {b}: s/a matched {on.round(2).tolist()} us, s' matched {tg.round(2).tolist()} us, "
+                  f"block end {us(td[b, :, 9].max()):.2f} us")
         nw = te[te > np.percentile(te, 99)]
         print(f"  slowest 1% TD waves end at {np.sort(nw).round(2).tolist()[-6:]} us")
         if rep == 2:   # per-segment medians (s_memtime cycles) of the critical waves
