@@ -161,7 +161,8 @@ def test_knn_graph_bit_exact(sw, N, k):
         assert torch.equal(mult[: B * N * N].view(B, N, N).cpu().float(), O.multiplicity_complete(B, N))
 
 
-@pytest.mark.parametrize("N,k", [(5, 3), (8, 5), (8, 2), (12, 5), (12, 10), (16, 7), (16, 15), (15, 9)])
+@pytest.mark.parametrize("N,k", [(2, 1), (3, 2), (4, 3), (5, 3), (8, 1), (8, 5), (8, 2), (12, 1), (12, 5), (12, 10),
+                                 (16, 7), (16, 15), (15, 9)])
 def test_acting_knn_ties_match_torch_topk(sw, golden_weights, N, k):
     """The acting path's kNN build (knn_masks_wave, boundary ties through the G-lane
     introselect restatement knn_tie_rows_wave) on tie-heavy formations: lattice positions in
@@ -185,7 +186,7 @@ def test_acting_knn_ties_match_torch_topk(sw, golden_weights, N, k):
     eng.act(push=False, full_out=True)
     torch.cuda.synchronize()
     assert torch.equal(mult.view(B, N, N).cpu().float(), O.multiplicity_knn(O.knn_sets(pos, k)))
-    if k < N:   # the tie path really ran: rows whose k-th and (k+1)-th distances are equal
+    if k < N and N >= 5:   # the tie path really ran: rows whose k-th and (k+1)-th distances are equal
         d = torch.linalg.norm(pos[:, None, :, :] - pos[:, :, None, :], dim=-1).sort(dim=-1).values
         assert int((d[..., k - 1] == d[..., k]).sum()) > B // 8
 
