@@ -152,6 +152,8 @@ def main():
             try:
                 peer = swdist.PeerExchange.connect(pg)
                 ok = peer.selftest()
+                if not ok and peer.error is not None:   # an IPC mapping failed on this rank
+                    why = str(peer.error)
             except RuntimeError as e:   # e.g. IPC unavailable
                 why, ok = str(e), False
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32,

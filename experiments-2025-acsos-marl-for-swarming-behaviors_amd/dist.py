@@ -95,6 +95,7 @@ class PeerExchange:
         for q, p in enumerate(recv):
             arr[q] = p
         self.struct = SwarmPeer(world_size, rank, arr, self.seq.data_ptr(), self.err.data_ptr(), int(timeout_us), 0)
+        self.error = None   # connect(): the first failed IPC mapping, if any
 
     # ------------------------------------------------------------------ construction
     @staticmethod
@@ -138,9 +139,11 @@ class PeerExchange:
             mapped.append(int(p.value))
         dist.barrier(group)
         end = cls(lib, W, r, own, [x or 0 for x in recv], dev, [own], mapped, timeout_us)
-        if err is not None:   # the caller falls back; the other ranks' self-tests expire on this one
-            end.close()
-            raise err
+        # a failed mapping does not raise here: this rank's buffer must stay allocated while the
+        # others (who mapped it) still run their self-test; selftest() then reports the failure
+        # on this rank without launching, and the others' waits expire on it (bench.py falls
+        # back to RCCL on every rank together)
+        end.error = err
         return end
 
     @classmethod
@@ -176,8 +179,11 @@ class PeerExchange:
 
     def selftest(self) -> bool:
         """Every rank contributes (rank + 1) * (1 + column): the rank-ordered sums are exact
-        small integers.  Returns False on a wrong sum or an expired wait (caller falls back)."""
+        small integers.  Returns False on a wrong sum, an expired wait or a failed IPC mapping at
+        connect() (caller falls back)."""
         from ._lib import N_PARAMS
+        if self.error is not None:
+            return False
         n = N_PARAMS + 1
         col = torch.arange(n, dtype=torch.float32, device=self.device)
         x = (self.rank + 1) * (1 + col)
