@@ -344,6 +344,26 @@ def main():
                 "hbm_frac": nbytes / t_k / 1e9 / PEAK_HBM_GBS,
                 "kernel_us": {k: round(v, 2) for k, v in kt.items()}}
 
+    # SURVEY §8(d)'s second number: acting-only (S = 0, frozen weights, eps 0, like
+    # Simulator.run_simulation) on the same engine and graph, one swarm_rollout launch per
+    # max_steps-tick episode; after the timed region, one GPU only
+    acting = None
+    if world == 1:
+        def rollouts(n):
+            for i in range(n):
+                eng.reset()
+                eng.rollout(max_steps, tick0=i * max_steps, eps=0.0)
+        rollouts(3)
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        rollouts(20)
+        torch.cuda.synchronize()
+        a_el = time.perf_counter() - a0
+        acting = {"value": round(B * N * 20 * max_steps / a_el, 1), "unit": "agent-steps/s",
+                  "us_per_tick": round(a_el / (20 * max_steps) * 1e6, 3),
+                  "step": f"reset + {max_steps}-tick rollout launch (swarm_rollout), 20 steps",
+                  "graph": args.graph}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
@@ -377,7 +397,7 @@ def main():
                            "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
                            "allreduce": allreduce,
                            "replicas_identical": replicas},
-                "roofline": roof, "cpu_baseline": cpu,
+                "roofline": roof, "cpu_baseline": cpu, "acting_only": acting,
                 "loss": ctrl["loss"]}
         print(json.dumps(line))
     if distributed:
