@@ -83,7 +83,12 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   WSmall<NS>& sm = SW[w].sm;
   const int c = d.c, p = d.p;
 
-  // prologue: every independent global load in flight at once
+  // prologue: every independent global load in flight at once.  The fused tick always learns
+  // (HO), so its optimizer-step operands are loaded first, from the preloaded pointers, ahead
+  // of anything that waits on ctrl or the kernarg segment
+  constexpr bool kLearnCT = MODE == MODE_TICK && NET == SWARM_NET_GCN && HO;
+  AdamRegs R;
+  if (kLearnCT) R.load(grad, w_cur, m_cur, v_cur, threadIdx.x);
   DFwd<NS> F;
   float px[CT], py[CT], vx[CT], vy[CT];
   bool valid[CT];
@@ -149,12 +154,11 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 #if SWARM_PIN
   asm volatile("" : "+s"(rp_s), "+s"(rp_sn), "+s"(rp_r), "+s"(rp_a), "+s"(o_rew), "+s"(o_avg), "+s"(o_hits), "+s"(smp));
 #endif
-  if (MODE == MODE_TICK && NET == SWARM_NET_GCN && A.learn) {
+  if (MODE == MODE_TICK && NET == SWARM_NET_GCN && (kLearnCT || A.learn)) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
     const int tid = threadIdx.x;
-    AdamRegs R;
-    R.load(grad, w_cur, m_cur, v_cur, tid);
+    if (!kLearnCT) R.load(grad, w_cur, m_cur, v_cur, tid);
     const uint32_t pending = cc.trained;
     const uint32_t tnow = cc.tick;
     const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;

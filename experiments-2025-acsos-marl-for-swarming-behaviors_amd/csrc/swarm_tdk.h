@@ -160,7 +160,10 @@ __device__ inline void drop_overrun(const bool (&okc)[DGeom<NS>::CT], bool (&dro
 template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
                                         const float* rs_next, const float* rr, const uint8_t* ra, int S, int B,
-                                        int N, int capacity, const TdArgs& A, const TdFused& X) {
+                                        int N, int capacity, const TdArgs& A, const TdFused& X,
+                                        const swarm_ctrl* __restrict__ ctrl_pre = nullptr, const float* g_pre = nullptr,
+                                        const float* w_pre = nullptr, const float* m_pre = nullptr,
+                                        const float* v_pre = nullptr) {
   constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;   // GPB: online (= target) waves per block
   constexpr int GPW = NS / GS;                             // graphs per wave
   constexpr int NT = 128 * GPB;
@@ -188,9 +191,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   //      valid (unused) rows.  Fused tick: the pending Adam step's operands and ctrl first.
   AdamRegs R;
   swarm_ctrl cc = {};
-  if (FUSED) {
-    R.load(X.lr.grad, X.lr.w_cur, X.lr.m_cur, X.lr.v_cur, threadIdx.x);
-    cc = *A.ctrl;
+  if (FUSED) {   // the fused kernel's preloaded argument SGPRs (== X.lr / A.ctrl): no kernarg round trip first
+    R.load(g_pre, w_pre, m_pre, v_pre, threadIdx.x);
+    cc = *ctrl_pre;
   }
   const uint32_t cap = (uint32_t)capacity;
   const uint32_t ring_graphs = cap * (uint32_t)B;

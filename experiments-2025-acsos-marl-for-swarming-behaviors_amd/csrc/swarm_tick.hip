@@ -32,16 +32,19 @@ union TickSmem {
 template <int NSA, int NST, int GS, int SCEN, int SPEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2 : 3, GS == 8 ? 2 : 3))) void tick_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
                                                    const float* grad, const float* w_cur, const float* m_cur,
-                                                   const float* v_cur, int B, int N, int n_act, ActArgs A,
+                                                   const float* v_cur, int B, int N, ActArgs A,
                                                    TdArgs T, TdFused X) {
   static_assert(64 * kActWPB == 256 && 128 * (kTdRows / NST) == 256, "one block shape for both halves");
   __shared__ TickSmem<NSA, NST> U;
+  // every argument the first round trip needs arrives preloaded in SGPRs (the leading 14
+  // dwords); the acting/TD split is derived from B instead of a 15th kernel argument
+  const int n_act = (B + kActWPB - 1) / kActWPB;
   if ((int)blockIdx.x < n_act)
     act_body<NSA, MODE_TICK, SCEN, SPEC, true>(U.a, blockIdx.x, n_act, ctrl, state, grad, w_cur, m_cur, v_cur, B, N,
                                                A);
   else
     td_body<NST, GS, SPEC, true>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next, T.replay.r,
-                                 T.replay.a, T.S, B, N, T.replay.capacity, T, X);
+                                 T.replay.a, T.S, B, N, T.replay.capacity, T, X, ctrl, grad, w_cur, m_cur, v_cur);
 }
 
 }  // namespace swarm
@@ -116,7 +119,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   // kNN / radius training graphs: the runtime-switched kernel
   const int spec = spec_of(cfg->graph, cfg->conv);
 #define SWARM_TICK_LAUNCH(NSA, GS, SC, SP) \
-  hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP>), grid, block, 0, st, ctrl, state, g, w, m, v, B, N, n_act, a, t, x)
+  hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP>), grid, block, 0, st, ctrl, state, g, w, m, v, B, N, a, t, x)
 #define SWARM_TICK_LAUNCH2(NSA, GS, SC)                                               \
   do {                                                                                 \
     if (spec == SPEC_COMPLETE_GAT) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GAT);  \
