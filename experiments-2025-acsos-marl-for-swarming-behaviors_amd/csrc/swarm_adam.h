@@ -65,7 +65,15 @@ struct AdamRegs {
       m[j] = reinterpret_cast<const float4*>(m_)[i];
       v[j] = reinterpret_cast<const float4*>(v_)[i];
     }
-    gt = grad[N_PARAMS - 1]; wt = w_[N_PARAMS - 1]; mt = m_[N_PARAMS - 1]; vt = v_[N_PARAMS - 1];
+    // the tail element as VECTOR loads (pointers moved into VGPRs): as scalar loads they were
+    // issued only after the wave's first scalar wait and arrived one round trip late
+    typedef const __attribute__((address_space(1))) float gfloat;   // global, not flat
+    gfloat* tg = (gfloat*)(grad + (N_PARAMS - 1));
+    gfloat* tw = (gfloat*)(w_ + (N_PARAMS - 1));
+    gfloat* tm = (gfloat*)(m_ + (N_PARAMS - 1));
+    gfloat* tv = (gfloat*)(v_ + (N_PARAMS - 1));
+    asm volatile("" : "+v"(tg), "+v"(tw), "+v"(tm), "+v"(tv));
+    gt = *tg; wt = *tw; mt = *tm; vt = *tv;
   }
 };
 

@@ -192,8 +192,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   AdamRegs R;
   swarm_ctrl cc = {};
   if (FUSED) {   // the fused kernel's preloaded argument SGPRs (== X.lr / A.ctrl): no kernarg round trip first
+    cc = *ctrl_pre;   // issued before any kernarg-segment load, so no wait on one delays it
+    __builtin_amdgcn_sched_barrier(0);
     R.load(g_pre, w_pre, m_pre, v_pre, threadIdx.x);
-    cc = *ctrl_pre;
+    __builtin_amdgcn_sched_barrier(0);   // every Adam operand load issued before the first scalar wait
   }
   const uint32_t cap = (uint32_t)capacity;
   const uint32_t ring_graphs = cap * (uint32_t)B;
