@@ -197,6 +197,17 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     R.load(g_pre, w_pre, m_pre, v_pre, threadIdx.x);
     __builtin_amdgcn_sched_barrier(0);   // every Adam operand load issued before the first scalar wait
   }
+  // fused: the scalars the sampling, the hand-off test and the optimizer step read (ctrl's
+  // write_slot, the batch size S, the Adam hyper-parameters) made opaque here, so they are
+  // loaded with the first scalar wait instead of being re-fetched at a later first use behind a
+  // second one (a kernarg / ctrl round trip on the TD chain)
+  swarm_adam_cfg hp = X.hp;
+  int32_t* sample_out = A.sample_out;
+  const unsigned long long* ho_rec = X.ho_rec;
+  if (FUSED) {
+    asm volatile("" : "+s"(cc.write_slot), "+s"(cc.trained), "+s"(S), "+s"(hp.beta1), "+s"(hp.beta2), "+s"(hp.eps),
+                 "+s"(hp.max_norm), "+s"(hp.update_target_every), "+s"(hp.world_size), "+s"(sample_out), "+s"(ho_rec));
+  }
   const uint32_t cap = (uint32_t)capacity;
   const uint32_t ring_graphs = cap * (uint32_t)B;
   int sid[CT];     // batch index of this lane's graph
@@ -258,10 +269,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     for (int q = threadIdx.x; q <= N_PARAMS; q += NT) slab_st(gslab(q), 0.0f);
     return;
   }
-  if (A.sample_out && online && p == 0) {
+  if (sample_out && online && p == 0) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
-      if (live[ct] && jl[ct] == 0) A.sample_out[sid[ct]] = (int32_t)gid[ct];
+      if (live[ct] && jl[ct] == 0) sample_out[sid[ct]] = (int32_t)gid[ct];
   }
   SWARM_STAMP(1);
   const bool waited = FUSED && __builtin_amdgcn_ballot_w64(wait) != 0;
@@ -271,9 +282,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   if (FUSED) {   // the pending optimizer step (train_gcn_dqn.py:125-133), as every acting block does;
                  // done before any hand-off wait so that none of it follows the wait
     const bool pending = cc.trained != 0u;
-    if (pending) adam_apply(R, X.hp, cc.adam_step_size, cc.adam_inv_bc2, threadIdx.x, L.red);
+    if (pending) adam_apply(R, hp, cc.adam_step_size, cc.adam_inv_bc2, threadIdx.x, L.red);
     store_w_lds(Pon, R, threadIdx.x);
-    if (pending && (cc.tick % (uint32_t)X.hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
+    if (pending && (cc.tick % (uint32_t)hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
     else ptg.store(Ptg, threadIdx.x);
     // waves whose graphs wait for a hand-off are the tick's critical path: top issue priority
     if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off):
@@ -286,7 +297,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         for (int ct = 0; ct < CT; ++ct) {
           okc[ct] = true;
           if (ho[ct]) {
-            const unsigned long long* rec = X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
+            const unsigned long long* rec = ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
             const int j = min(jl[ct], N - 1);
             const unsigned long long* sp = rec + (online ? 0 : 4 * N) + 4 * j;
             const unsigned long long g0 = ld_granule(sp), g1 = ld_granule(sp + 1), g2 = ld_granule(sp + 2),
@@ -342,7 +353,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       for (int ct = 0; ct < CT; ++ct) {
         okc[ct] = true;
         if (ho[ct] && !live_drop[ct]) {
-          const unsigned long long g = ld_granule(X.ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) +
+          const unsigned long long g = ld_granule(ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) +
                                                   8 * N + min(jl[ct], N - 1));
           okc[ct] = !kHoForceDrop && (uint32_t)(g >> 32) == tag;
           ok = ok && okc[ct];
