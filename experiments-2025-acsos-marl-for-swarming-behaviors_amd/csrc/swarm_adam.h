@@ -139,9 +139,12 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float 
   float nn = red[0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) nn = nn + red[w];
-  const float total_norm = sqrtf(nn);
+  // v_sqrt_f32 and a reciprocal multiply (<= 1 ulp each) instead of the correctly rounded
+  // expansions: the clip coefficient is a serial chain every prologue waits on (0.075 us per
+  // tick at C2, profiles/r02_ab_wpe.jsonl)
+  const float total_norm = __builtin_amdgcn_sqrtf(nn);
   AD_STAMP(1);
-  const float coef = hp.max_norm / (total_norm + 1e-6f);
+  const float coef = hp.max_norm * __builtin_amdgcn_rcpf(total_norm + 1e-6f);
   const float clamped = coef < 1.0f ? coef : 1.0f;
   const float bc2_sqrt = inv_bc2_sqrt;   // reciprocal of sqrt(bias_correction2)
   const float one_m_b1 = (float)(1.0 - (double)hp.beta1);
