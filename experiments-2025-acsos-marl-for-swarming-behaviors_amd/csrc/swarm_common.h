@@ -300,15 +300,20 @@ static __constant__ unsigned long long* g_swarm_stamps;
 #endif
 
 // compile-time graph / conv specialisations of the act and TD kernels
-enum { SPEC_RUNTIME = 0, SPEC_COMPLETE_GAT = 1, SPEC_COMPLETE_GCN = 2, SPEC_KNN_GAT = 3 };
+// (SPEC_RADIUS_GAT: the north_star's radius-neighbour graph, GoTo training ticks of <= 8 agents)
+enum { SPEC_RUNTIME = 0, SPEC_COMPLETE_GAT = 1, SPEC_COMPLETE_GCN = 2, SPEC_KNN_GAT = 3, SPEC_RADIUS_GAT = 4 };
 __host__ __device__ inline int spec_of(int graph, int conv) {
   if (graph == SWARM_GRAPH_COMPLETE) return conv == SWARM_CONV_GAT ? SPEC_COMPLETE_GAT : SPEC_COMPLETE_GCN;
   if (graph == SWARM_GRAPH_KNN && conv == SWARM_CONV_GAT) return SPEC_KNN_GAT;
+  if (graph == SWARM_GRAPH_RADIUS && conv == SWARM_CONV_GAT) return SPEC_RADIUS_GAT;
   return SPEC_RUNTIME;
 }
 template <int SPEC>
 __device__ inline int spec_graph(int runtime) {
-  return SPEC == SPEC_RUNTIME ? runtime : (SPEC == SPEC_KNN_GAT ? (int)SWARM_GRAPH_KNN : (int)SWARM_GRAPH_COMPLETE);
+  return SPEC == SPEC_RUNTIME       ? runtime
+         : SPEC == SPEC_KNN_GAT     ? (int)SWARM_GRAPH_KNN
+         : SPEC == SPEC_RADIUS_GAT  ? (int)SWARM_GRAPH_RADIUS
+                                    : (int)SWARM_GRAPH_COMPLETE;
 }
 template <int SPEC>
 __device__ inline int spec_conv(int runtime) {

@@ -115,8 +115,9 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   hipStream_t st = (hipStream_t)stream;
   const float *g = lr->grad, *w = lr->w_cur, *m = lr->m_cur, *v = lr->v_cur;
   const bool oa = cfg->scenario == SWARM_OBSTACLE_AVOIDANCE;
-  // complete graph (the reference's training graph): graph and conv fixed at compile time;
-  // kNN / radius training graphs: the runtime-switched kernel
+  // complete graph (the reference's training graph) and GoTo's radius graph with GAT (the
+  // north_star graph, N <= 8): graph and conv fixed at compile time; others: the
+  // runtime-switched kernel
   const int spec = spec_of(cfg->graph, cfg->conv);
 #define SWARM_TICK_LAUNCH(NSA, GS, SC, SP) \
   hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP>), grid, block, 0, st, ctrl, state, g, w, m, v, B, N, a, t, x)
@@ -130,6 +131,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   if (N <= 8) {
     if (fl) SWARM_TICK_LAUNCH2(8, 8, SWARM_FLOCKING);
     else if (oa) SWARM_TICK_LAUNCH2(8, 8, SWARM_OBSTACLE_AVOIDANCE);
+    else if (spec == SPEC_RADIUS_GAT) SWARM_TICK_LAUNCH(8, 8, SWARM_GOTO, SPEC_RADIUS_GAT);
     else SWARM_TICK_LAUNCH2(8, 8, SWARM_GOTO);
   } else {
     if (fl) SWARM_TICK_LAUNCH2(16, 16, SWARM_FLOCKING);

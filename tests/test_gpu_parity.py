@@ -535,6 +535,9 @@ def test_fused_tick_equals_unfused(sw, golden_weights, scen, N, graph, conv):
                                                         ("GoTo", 8, "gcn", 1024, 977, "complete"),
                                                         ("GoTo", 8, "gat", 64, 2, "knn"),
                                                         ("ObstacleAvoidance", 12, "gat", 48, 2, "radius"),
+                                                        # GoTo radius + GAT: the specialised tick kernel
+                                                        ("GoTo", 8, "gat", 64, 2, "radius"),
+                                                        ("GoTo", 6, "gat", 40, 1, "radius"),
                                                         ("GoTo", 5, "gat", 37, 3, "complete"),      # ragged blocks
                                                         ("ObstacleAvoidance", 11, "gcn", 33, 2, "knn"),
                                                         ("Flocking", 8, "gat", 64, 2, "complete"),

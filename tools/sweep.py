@@ -26,7 +26,7 @@ RUNS += [
     ("C2 GoTo 8x1024 GAT act complete", ["--mode", "act"]),
     ("C3 OA 12x1024 GAT act kNN-10", ["--mode", "act", "--scenario", "ObstacleAvoidance", "--agents", "12",
                                       "--graph", "knn", "--knn-k", "10"]),
-    # the north_star's radius-neighbour graph (not in the reference; 3-launch tick for training)
+    # the north_star's radius-neighbour graph (not in the reference; fused tick, radius + GAT specialised)
     ("C2 GoTo 8x1024 GAT act radius-0.3", ["--mode", "act", "--graph", "radius", "--radius", "0.3"]),
     ("C2 GoTo 8x1024 GAT train radius-0.3", ["--graph", "radius", "--radius", "0.3"]),
     # the Flocking scenario (one-layer GCN training, as train_model('Flocking'))
