@@ -160,11 +160,13 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   const dim3 grid((tiles + kActWPB - 1) / kActWPB), block(64 * kActWPB);
   const float *g = a.lr.grad, *w = a.lr.w_cur, *m = a.lr.m_cur, *v = a.lr.v_cur;
   // specialised kernels for the training tick (complete graph, GAT or GCN) and the rollout
-  // (those two plus kNN + GAT, the Simulator's graph); everything else runs SPEC_RUNTIME
+  // (those two plus kNN + GAT, the Simulator's graph, and GoTo's radius + GAT, the north_star
+  // graph); everything else runs SPEC_RUNTIME
   constexpr bool kTick = MODE == MODE_TICK || MODE == MODE_ROLLOUT;
   constexpr int S1 = kTick ? SPEC_COMPLETE_GAT : SPEC_RUNTIME;
   constexpr int S2 = kTick ? SPEC_COMPLETE_GCN : SPEC_RUNTIME;
   constexpr int S3 = MODE == MODE_ROLLOUT ? SPEC_KNN_GAT : SPEC_RUNTIME;
+  constexpr int S4 = MODE == MODE_ROLLOUT ? SPEC_RADIUS_GAT : SPEC_RUNTIME;   // GoTo, N <= 8 only
   const int spec = kTick ? spec_of(a.graph, a.conv) : SPEC_RUNTIME;
 #define SWARM_ACT_LAUNCH1(NS, SC, SP) \
   hipLaunchKernelGGL((act_kernel<NS, MODE, SC, SP>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
@@ -198,7 +200,10 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   }
   }
   if (a.N <= 8) {
-    if (fl) SWARM_ACT_LAUNCH1(8, FL, SPEC_RUNTIME); else if (oa) SWARM_ACT_LAUNCH(8, OA); else SWARM_ACT_LAUNCH(8, SWARM_GOTO);
+    if (fl) SWARM_ACT_LAUNCH1(8, FL, SPEC_RUNTIME);
+    else if (oa) SWARM_ACT_LAUNCH(8, OA);
+    else if (spec == SPEC_RADIUS_GAT) SWARM_ACT_LAUNCH1(8, SWARM_GOTO, S4);
+    else SWARM_ACT_LAUNCH(8, SWARM_GOTO);
   } else if (a.N <= 16) {
     if (fl) SWARM_ACT_LAUNCH1(16, FL, SPEC_RUNTIME); else if (oa) SWARM_ACT_LAUNCH(16, OA); else SWARM_ACT_LAUNCH(16, SWARM_GOTO);
   } else {

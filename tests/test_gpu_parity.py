@@ -350,11 +350,15 @@ def _act_tick_case(sw, golden_weights, scen, N, graph, k, conv):
         assert torch.equal(eng.rep_s1[0].cpu(), eng.state.cpu())
 
 
-def test_rollout_equals_single_ticks(sw, golden_weights):
+@pytest.mark.parametrize("graph", ["knn", "radius", "complete"])
+def test_rollout_equals_single_ticks(sw, golden_weights, graph):
+    """The rollout launch (specialised kernels: kNN / radius / complete + GAT) == single act
+    ticks of the runtime-switched kernel."""
     B, N, T = 64, 8, 12
     p = _params(golden_weights, "go_to", 3)
-    a = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, graph="knn", knn_k=5, learn=False, eps=0.0)
-    b = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, graph="knn", knn_k=5, learn=False, eps=0.0)
+    kw = dict(seed=4, params=p, graph=graph, knn_k=5, radius=0.3, learn=False, eps=0.0)
+    a = sw.SwarmEngine("GoTo", N, B, **kw)
+    b = sw.SwarmEngine("GoTo", N, B, **kw)
     a.reset(0)
     b.reset(0)
     rew = torch.zeros(B, N, device="cuda")
