@@ -17,8 +17,10 @@ import swarm_amd  # noqa: E402
 from swarm_amd import _lib  # noqa: E402
 from tools.stamps import ACT, ACT_ORDER, TD, report  # noqa: E402
 
-TD_WAIT = {**TD, 10: "hand-off (granules matched)", 2: "B0 barrier"}
-TD_WAIT_ORDER = [0, 1, 10, 2, 16, 17, 18, 19, 20, 3, 4, 5, 24, 25, 27, 6, 7]
+# stamp 10 (granules matched) is a 100 MHz realtime stamp, reported in us above; the cycle
+# segments run from 1 straight to 2, i.e. the hand-off wait plus the B0 barrier
+TD_WAIT = {**TD, 2: "Adam + hand-off wait + B0 barrier"}
+TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 24, 25, 27, 6, 7]
 
 
 def main():
