@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3     # MI355X FP32 MFMA (= vector) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0        # HBM3E spec
+PEAK_CLOCK_GHZ = 2.4         # the clock the FP32 peak is quoted at (1024 SIMDs x 64 FLOP/cycle)
 
 
 def gat_fwd_flops(N: int, avg_in_degree: float) -> float:
@@ -112,13 +113,16 @@ def parse():
                     help="gat3: the Flocking checkpoints' three-layer GAT (acting only, --mode act)")
     ap.add_argument("--batch", type=int, default=None, help="sampled graphs per update per GPU (default = envs)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                     "gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--force-dist", action="store_true",
                     help="rehearsal: create the process group and run the gradient all-reduce even at 1 rank")
+    ap.add_argument("--no-compare-rccl", dest="compare_rccl", action="store_false",
+                    help="N > 1 with the peer exchange: skip the second timed region over RCCL")
+    ap.add_argument("--c1-seconds", type=float, default=5.0, help="CPU sample of BASELINE configs[0] (C1)")
     ap.add_argument("--allreduce", default="auto", choices=("auto", "peer", "rccl"),
                     help="gradient all-reduce for N > 1: peer = xGMI stores fused into the slab reduce "
                          "(swarm_reduce_advance_peer); rccl = torch.distributed all_reduce after it; auto = peer "
@@ -154,7 +158,7 @@ def main():
                 ok = peer.selftest()
                 if not ok and peer.error is not None:   # an IPC mapping failed on this rank
                     why = str(peer.error)
-            except RuntimeError as e:   # e.g. IPC unavailable
+            except (RuntimeError, ValueError) as e:   # IPC unavailable; W > SWARM_PEER_MAX (every rank alike)
                 why, ok = str(e), False
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
                                 device="cuda" if args.backend == "nccl" else "cpu")
@@ -202,57 +206,88 @@ def main():
         else:
             eng.train_tick3(full_out=False)
 
-    graph = None
-    if not args.no_graph and (not distributed or args.backend == "nccl" or peer is not None):
-        tick()                              # eager warm tick (and first RCCL all-reduce) before capture
-        try:
-            graph = eng.capture(max_steps, tick)   # one episode's ticks
-        except RuntimeError as e:           # e.g. a collective that refuses stream capture
-            print(f"[bench] rank {rank}: hipGraph capture failed ({e}); eager ticks", file=sys.stderr)
-            graph = None
-        if distributed:                     # every rank runs the same launch mode
-            ok = torch.tensor([1 if graph is not None else 0], dtype=torch.int32,
-                              device="cuda" if args.backend == "nccl" else "cpu")
-            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
-            if int(ok.item()) == 0:
-                graph = None
     stream = torch.cuda.current_stream()
 
-    def episode():   # one step: reset_world_at, then max_steps ticks
-        eng.reset()
-        if graph is not None:
-            graph.replay()
-        else:
-            for _ in range(max_steps):
-                tick()
+    def timed_region():
+        """capture one episode's ticks (hipGraph), W warmup steps, then K timed steps between a
+        barrier + synchronize on both sides; returns (max-over-ranks seconds, tick spread, graph?)"""
+        graph = None
+        if not args.no_graph and (not distributed or args.backend == "nccl" or eng.peer is not None):
+            tick()                              # eager warm tick (and first RCCL all-reduce) before capture
+            try:
+                graph = eng.capture(max_steps, tick)   # one episode's ticks
+            except RuntimeError as e:           # e.g. a collective that refuses stream capture
+                print(f"[bench] rank {rank}: hipGraph capture failed ({e}); eager ticks", file=sys.stderr)
+                graph = None
+            if distributed:                     # every rank runs the same launch mode
+                ok = torch.tensor([1 if graph is not None else 0], dtype=torch.int32,
+                                  device="cuda" if args.backend == "nccl" else "cpu")
+                torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+                if int(ok.item()) == 0:
+                    graph = None
 
-    for _ in range(args.warmup):
-        episode()
-    torch.cuda.synchronize()
-    if distributed:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    t0 = time.perf_counter()
-    evs[0].record(stream)
-    for i in range(args.steps):
-        episode()
-        evs[i + 1].record(stream)
-    torch.cuda.synchronize()
-    if distributed:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ep_us = [evs[i].elapsed_time(evs[i + 1]) * 1e3 / max_steps for i in range(args.steps)]
-    tick_spread = ({"median": round(float(np.median(ep_us)), 3), "min": round(min(ep_us), 3),
-                    "max": round(max(ep_us), 3), "per": "episode of %d ticks, HIP events" % max_steps}
-                   if ep_us else None)
-    if distributed:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        def episode():   # one step: reset_world_at, then max_steps ticks
+            eng.reset()
+            if graph is not None:
+                graph.replay()
+            else:
+                for _ in range(max_steps):
+                    tick()
+
+        for _ in range(args.warmup):
+            episode()
+        torch.cuda.synchronize()
+        if distributed:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        t0 = time.perf_counter()
+        evs[0].record(stream)
+        for i in range(args.steps):
+            episode()
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        if distributed:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ep_us = [evs[i].elapsed_time(evs[i + 1]) * 1e3 / max_steps for i in range(args.steps)]
+        spread = ({"median": round(float(np.median(ep_us)), 3), "min": round(min(ep_us), 3),
+                   "max": round(max(ep_us), 3), "per": "episode of %d ticks, HIP events" % max_steps}
+                  if ep_us else None)
+        if distributed:
+            t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, spread, graph
+
+    elapsed, tick_spread, graph = timed_region()
+    # N > 1 with the peer exchange: the same workload again with the RCCL all-reduce after the
+    # slab reduce (north_star's "single RCCL all-reduce over xGMI"), so one run reports both paths
+    both = None
+    if distributed and peer is not None and args.backend == "nccl" and args.compare_rccl:
+        peer.check()
+        el_peer = elapsed
+        eng.peer = None
+        el_rccl, spread_rccl, g_rccl = timed_region()
+        eng.peer = peer
+        both = {"peer": {"value": round(B * N * world * args.steps * max_steps / el_peer, 1),
+                         "us_per_tick": round(el_peer / (args.steps * max_steps) * 1e6, 3)},
+                "rccl": {"value": round(B * N * world * args.steps * max_steps / el_rccl, 1),
+                         "us_per_tick": round(el_rccl / (args.steps * max_steps) * 1e6, 3),
+                         "tick_us": spread_rccl, "hipgraph": g_rccl is not None},
+                "headline": "peer"}
     ctrl = eng.read_ctrl()
     assert ctrl["trained"] == 1 and math.isfinite(ctrl["loss"]), ctrl
+    rank_errors = None
+    if distributed:   # every rank's fused-tick hand-off overruns and expired exchange waits (0 in a correct run)
+        e = torch.tensor([eng.handoff_errors(), peer.errors() if peer is not None else 0,
+                          int(eng.ctrl[23].item())], dtype=torch.int64,
+                         device="cuda" if args.backend == "nccl" else "cpu")
+        allv = [torch.zeros_like(e) for _ in range(world)]
+        torch.distributed.all_gather(allv, e)
+        rank_errors = [{"rank": q, "handoff_overruns": int(v[0]), "peer_wait_expired": int(v[1]),
+                        "peer_hold": int(v[2])} for q, v in enumerate(allv)]
     if peer is not None:
         peer.check()   # an expired exchange wait would have summed a wrong gradient: fail loudly
     replicas = None
@@ -330,18 +365,26 @@ def main():
             flops, nbytes = td_flops_launch, S * N * 37
             kname, pmcf = "td_kernel (swarm_td_grad)", "r01_pmc_td.json"
         ach = flops / t_k / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", pmcf.replace("r01_", "r02_"))   # this round's passes if present
-        if not os.path.exists(pmc):
-            pmc = os.path.join(ROOT, "profiles", pmcf)
-        if os.path.exists(pmc) and headline:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        traffic, mfma_util, pmc_src = None, None, None
+        for rnd in ("r03_", "r02_", "r01_"):   # the newest round's PMC passes (scripts/pmc.sh)
+            pmc = os.path.join(ROOT, "profiles", pmcf.replace("r01_", rnd))
+            if os.path.exists(pmc) and headline:
+                d = json.load(open(pmc))
+                traffic = d.get("hbm_bytes_per_launch")
+                kk = d.get("kernels", {}).get(d.get("kernel", ""), {}).get("counters", {})
+                busy = kk.get("SQ_VALU_MFMA_BUSY_CYCLES")
+                if busy is not None:   # MFMA pipe cycles / (1024 SIMDs x this launch's time at the 2.4 GHz peak clock)
+                    mfma_util = busy / (1024 * PEAK_CLOCK_GHZ * 1e9 * t_k)
+                pmc_src = os.path.basename(pmc)
+                break
         roof = {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
                 "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": kname,
                 "algorithmic_flops_per_launch": flops,
                 "algorithmic_bytes_per_launch": nbytes,
                 "hbm_frac": nbytes / t_k / 1e9 / PEAK_HBM_GBS,
+                "hbm_gbs": round(traffic / t_k / 1e9, 1) if traffic else None,
+                "mfma_util": mfma_util, "pmc": pmc_src,
                 "kernel_us": {k: round(v, 2) for k, v in kt.items()}}
 
     # SURVEY §8(d)'s second number: acting-only (S = 0, frozen weights, eps 0, like
@@ -366,19 +409,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import cpu_baseline
-        threads = min(16, os.cpu_count() or 1)
-        torch.set_num_threads(threads)
-        sid = 0 if scen == "GoTo" else 1
-        r = cpu_baseline.vectorized_train(w0, sid, B, N, S, seconds=args.cpu_seconds)
-        r1 = cpu_baseline.reference_shaped_train(w0, sid, N, seconds=max(3.0, args.cpu_seconds / 3))
-        cpu = {"value": round(r["agent_steps_per_s"], 1), "unit": "agent-steps/s", "cores": threads,
-               "kind": "port",
-               "sample": f"vectorised PyTorch-CPU oracle, same workload ({B} envs x {N} agents, S={S}), "
-                         f"{r['ticks']} ticks in {r['seconds']:.1f}s on {threads} threads ({platform.processor() or 'x86_64'})",
-               "reference_shaped_b1": {"value": round(r1["agent_steps_per_s"], 1),
-                                       "sample": f"B=1 loop shaped like train_gcn_dqn.py:153-178 (S=32), "
-                                                 f"{r1['ticks']} ticks in {r1['seconds']:.1f}s"}}
+        cpu = cpu_baseline_leg(args, w0, scen, B, N, S, eng)
 
     if rank == 0:
         line = {"metric": "env-steps/sec (agents×envs), GoTo 8 agents×1024 envs @1/2/4/8 GPU",
@@ -395,13 +426,97 @@ def main():
                                           " + xGMI peer grad all-reduce" if peer is not None else
                                           f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce"),
                            "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
-                           "allreduce": allreduce,
+                           "allreduce": allreduce, "allreduce_paths": both, "rank_errors": rank_errors,
                            "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu, "acting_only": acting,
                 "loss": ctrl["loss"]}
         print(json.dumps(line))
     if distributed:
         torch.distributed.destroy_process_group()
+
+
+def host_cpu():
+    """The host's CPU as the process sees it: model name (/proc/cpuinfo), os.cpu_count(), the
+    CPUs this process may run on (sched_getaffinity) and the cgroup CPU quota, if any."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    n = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = n
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"model": model or platform.processor() or "unknown", "os_cpu_count": n, "affinity": aff,
+            "cgroup_quota_cpus": quota}
+
+
+def cpu_baseline_leg(args, w0, scen, B, N, S, eng):
+    """SURVEY §8(d) CPU baseline on the GPU box's host cores (after the timed region; rank 0,
+    N = 1): the vectorised PyTorch-CPU oracle on a bounded sample of the same workload, at the
+    thread count the process may use (affinity / cgroup quota) and at os.cpu_count() threads
+    when that differs (the faster is reported: no throttled baseline); the reference-shaped
+    B = 1 training loop; and BASELINE.json configs[0] (C1: GoTo, 5 agents, 1 env, the
+    evaluation script's loop with kNN-5) beside this framework's GPU at that same shape."""
+    from oracle import cpu_baseline
+    info = host_cpu()
+    usable = info["affinity"]
+    if info["cgroup_quota_cpus"]:
+        usable = max(1, min(usable, math.ceil(info["cgroup_quota_cpus"])))
+    counts = sorted({usable, info["os_cpu_count"]})
+    sid = 0 if scen == "GoTo" else 1
+    sweep = []
+    for th in counts:
+        torch.set_num_threads(th)
+        r = cpu_baseline.vectorized_train(w0, sid, B, N, S, seconds=args.cpu_seconds)
+        sweep.append({"threads": th, "value": round(r["agent_steps_per_s"], 1), "ticks": r["ticks"],
+                      "seconds": round(r["seconds"], 2)})
+    best = max(sweep, key=lambda x: x["value"])
+    torch.set_num_threads(best["threads"])
+    r1 = cpu_baseline.reference_shaped_train(w0, sid, N, seconds=max(3.0, args.cpu_seconds / 3))
+    wgo = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))["weights_go_to"][0])
+    c1 = cpu_baseline.reference_shaped_eval(wgo, 0, 5, 5, seconds=args.c1_seconds)
+    # the same C1 shape on the GPU: one env, 5 agents, kNN-5, greedy, 50-tick episodes, each
+    # episode one swarm_rollout launch
+    import swarm_amd
+    e1 = swarm_amd.SwarmEngine("GoTo", 5, 1, seed=0, params=wgo, graph="knn", knn_k=5, learn=False, eps=0.0)
+    for i in range(3):
+        e1.reset()
+        e1.rollout(50, tick0=50 * i, eps=0.0)
+    torch.cuda.synchronize()
+    g0 = time.perf_counter()
+    for i in range(40):
+        e1.reset()
+        e1.rollout(50, tick0=50 * i, eps=0.0)
+    torch.cuda.synchronize()
+    g_el = time.perf_counter() - g0
+    return {"value": best["value"], "unit": "agent-steps/s", "cores": best["threads"], "kind": "port",
+            "sample": f"vectorised PyTorch-CPU oracle, same workload ({B} envs x {N} agents, S={S}), "
+                      f"{best['ticks']} ticks in {best['seconds']:.1f}s on {best['threads']} threads",
+            "host": info, "thread_sweep": sweep,
+            "reference_shaped_b1": {"value": round(r1["agent_steps_per_s"], 1), "threads": best["threads"],
+                                    "sample": f"B=1 loop shaped like train_gcn_dqn.py:153-178 (S=32), "
+                                              f"{r1['ticks']} ticks in {r1['seconds']:.1f}s"},
+            "c1": {"config": "BASELINE.json configs[0]: GoTo, 5 agents, 1 env, CPU PyTorch reference "
+                             "(tests/ script shape: simulator.py:47-109 with kNN-5, 50-tick episodes)",
+                   "value": round(c1["agent_steps_per_s"], 1), "unit": "agent-steps/s",
+                   "threads": best["threads"], "sample": f"{c1['ticks']} ticks in {c1['seconds']:.1f}s",
+                   "gpu_same_shape": {"value": round(5 * 50 * 40 / g_el, 1), "unit": "agent-steps/s",
+                                      "us_per_tick": round(g_el / (50 * 40) * 1e6, 3),
+                                      "sample": "40 episodes, reset + one 50-tick swarm_rollout launch each"}}}
 
 
 def bench_act(args, eng, world, rank, distributed, max_steps):

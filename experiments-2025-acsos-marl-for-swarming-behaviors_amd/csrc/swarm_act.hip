@@ -4,7 +4,7 @@
 // Reference call sites replaced (paths relative to the reference checkout):
 //   train_gcn_dqn.py:161-172   graph -> model -> eps-greedy -> env.step -> replay.push
 //   simulator.py:59-93         kNN graph -> argmax -> env.step -> metrics
-//   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:242-321
+//   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:94-173
 #include <stdlib.h>
 
 #include "swarm_actk.h"

@@ -5,7 +5,7 @@
 // Reference call sites replaced (paths relative to the reference checkout):
 //   train_gcn_dqn.py:161-172   graph -> model -> eps-greedy -> env.step -> replay.push
 //   simulator.py:59-93         kNN graph -> argmax -> env.step -> metrics
-//   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:242-321
+//   go_to_position_scenario.py:83-132, obstacle_avoidance_scenario.py:94-173
 #pragma once
 #include "swarm_adam.h"
 #include "swarm_env.h"
@@ -159,7 +159,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
     const int tid = threadIdx.x;
     if (!kLearnCT) R.load(grad, w_cur, m_cur, v_cur, tid);
-    const uint32_t pending = cc.trained;
+    const uint32_t pending = cc.peer_hold ? 0u : cc.trained;   // a held rank applies no step
     const uint32_t tnow = cc.tick;
     const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;
     float gn = 0.0f;

@@ -28,7 +28,7 @@ constexpr int kFeat = 7;
 constexpr int kActions = 9;
 
 constexpr float kGoalX = -0.8f, kGoalY = 0.8f;      // go_to_position_scenario.py:86
-constexpr float kObstX = -0.1f, kObstY = 0.1f;      // obstacle_avoidance_scenario.py:247
+constexpr float kObstX = -0.1f, kObstY = 0.1f;      // obstacle_avoidance_scenario.py:99
 constexpr float kRadius = 0.05f;                    // VMAS Sphere() default radius
 constexpr float kCollisionForce = 100.0f;           // VMAS World collision_force
 constexpr float kContactMargin = 0.001f;            // VMAS World contact_margin

@@ -34,9 +34,9 @@ __device__ inline void peer_put(void* buf, int region, uint32_t parity, int src,
 }
 
 // poll this rank's own (uncached) buffer until the granule carries `tag`; bounded by the chip's
-// 100 MHz clock, an expired wait counts in *err and yields 0
+// 100 MHz clock, an expired wait counts in *err, sets *expired and yields 0
 __device__ inline float peer_wait(void* own, int region, uint32_t parity, int src, int col, uint32_t tag,
-                                  int32_t* err, uint32_t timeout_us) {
+                                  int32_t* err, uint32_t timeout_us, bool* expired) {
   const unsigned long long* g = peer_slot(own, region, parity, src, col);
   unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if ((uint32_t)(v >> 32) != tag) {
@@ -48,6 +48,7 @@ __device__ inline float peer_wait(void* own, int region, uint32_t parity, int sr
       if ((uint32_t)(v >> 32) == tag) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
         atomicAdd(err, 1);
+        *expired = true;
         return 0.0f;
       }
     }
@@ -58,19 +59,28 @@ __device__ inline float peer_wait(void* own, int region, uint32_t parity, int sr
 // The exchange of one column block: `mine` = this rank's value of column `col` (valid in the
 // threads with q == 0 via the LDS row `mine_l`), threads q < W publish it to rank q and collect
 // rank q's value; the caller then sums rv[0..W) in rank order.  blockDim = kCols * (>= W) threads
-// indexed (q = tid / kCols, c = tid % kCols).  Ends with a block barrier.
+// indexed (q = tid / kCols, c = tid % kCols).  Ends with a block barrier.  hold != nullptr
+// (swarm_reduce_advance_peer: &ctrl->peer_hold): an expired wait of the block sets it to 1.
 template <int kCols>
 __device__ inline void peer_exchange(const swarm_peer& P, int region, int blk, int q, int c, int col, int ncols,
-                                     const float* mine_l, float (*rv)[kCols]) {
+                                     const float* mine_l, float (*rv)[kCols], uint32_t* hold = nullptr) {
+  __shared__ int any_expired;
   const uint32_t s = P.seq[region * kPeerSeqRegion + blk];
   const uint32_t tag = s + 1u, parity = s & 1u;
   const int W = P.world_size;
+  if (threadIdx.x == 0) any_expired = 0;
+  __syncthreads();
   if (q < W && col < ncols) {
+    bool expired = false;
     peer_put(P.recv[q], region, parity, P.rank, col, tag, mine_l[c]);
-    rv[q][c] = peer_wait(P.recv[P.rank], region, parity, q, col, tag, P.err, P.timeout_us);
+    rv[q][c] = peer_wait(P.recv[P.rank], region, parity, q, col, tag, P.err, P.timeout_us, &expired);
+    if (expired) any_expired = 1;
   }
   __syncthreads();
-  if (threadIdx.x == 0) P.seq[region * kPeerSeqRegion + blk] = s + 1u;
+  if (threadIdx.x == 0) {
+    P.seq[region * kPeerSeqRegion + blk] = s + 1u;
+    if (hold && any_expired) *hold = 1u;   // sticky; read by the next launch's optimizer step
+  }
 }
 
 // host-side argument check of the peer entry points

@@ -82,7 +82,9 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     uint32_t nk_n = 0, nk_tick = 0;
     const uint32_t cap = (uint32_t)A.capacity;
     if (t == 0) {
-      c_trained = C->trained; c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
+      // a held rank (peer_hold: an expired exchange wait) applied no step this tick
+      c_trained = C->peer_hold ? 0u : C->trained;
+      c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
       b1p = ctrl_get_double(C, CTRL_B1POW);
       b2p = ctrl_get_double(C, CTRL_B2POW);
       if (c_trained) {   // the step this tick's act kernel applied
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   }
   if (PEER) {
     __syncthreads();
-    peer_exchange<kRedCols>(A.peer, 0, blockIdx.x, q, c, col, N_PARAMS + 1, part[0], peer_rv);
+    peer_exchange<kRedCols>(A.peer, 0, blockIdx.x, q, c, col, N_PARAMS + 1, part[0], peer_rv, &C->peer_hold);
     if (q == 0 && col <= N_PARAMS) {
       float tot = peer_rv[0][c];
       for (int w = 1; w < A.peer.world_size; ++w) tot = tot + peer_rv[w][c];
@@ -208,7 +210,8 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
   const uint32_t tick = C->tick;
   const uint32_t step = C->adam_step + 1;
   const float step_size = C->adam_step_size, inv_bc2 = C->adam_inv_bc2;
-  const bool train = A.flush ? (C->trained != 0u) : (valid_slots * (uint32_t)A.B >= (uint32_t)A.hp.batch);
+  const bool train = A.flush ? (C->trained != 0u && C->peer_hold == 0u)
+                             : (valid_slots * (uint32_t)A.B >= (uint32_t)A.hp.batch);
   // target sync: unfused = after the TD step of tick `tick` ((tick+1) % every); flush = the
   // fused tick already advanced ctrl, so the pending update belongs to tick - 1
   const bool sync = ((A.flush ? tick : tick + 1) % (uint32_t)A.hp.update_target_every) == 0u;

@@ -281,7 +281,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   for (int ct = 0; ct < CT; ++ct) live_drop[ct] = false;
   if (FUSED) {   // the pending optimizer step (train_gcn_dqn.py:125-133), as every acting block does;
                  // done before any hand-off wait so that none of it follows the wait
-    const bool pending = cc.trained != 0u;
+    const bool pending = cc.trained != 0u && cc.peer_hold == 0u;   // a held rank applies no step
     if (pending) adam_apply(R, hp, cc.adam_step_size, cc.adam_inv_bc2, threadIdx.x, L.red);
     store_w_lds(Pon, R, threadIdx.x);
     if (pending && (cc.tick % (uint32_t)hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);

@@ -17,6 +17,13 @@
 #include "swarm_actk.h"
 #include "swarm_tdk.h"
 
+// A/B knob (tools/ab_build.py only; 0 in every shipped library): TD blocks sleep
+// SWARM_TD_DELAY x 1024 cycles before their first loads, so the acting blocks' prologue
+// (the hand-off graphs' critical path) has the memory system to itself
+#ifndef SWARM_TD_DELAY
+#define SWARM_TD_DELAY 0
+#endif
+
 namespace swarm {
 
 template <int NSA, int NST>
@@ -42,9 +49,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2
   if ((int)blockIdx.x < n_act)
     act_body<NSA, MODE_TICK, SCEN, SPEC, true>(U.a, blockIdx.x, n_act, ctrl, state, grad, w_cur, m_cur, v_cur, B, N,
                                                A);
-  else
+  else {
+    for (int i = 0; i < SWARM_TD_DELAY; ++i) __builtin_amdgcn_s_sleep(16);
     td_body<NST, GS, SPEC, true>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next, T.replay.r,
                                  T.replay.a, T.S, B, N, T.replay.capacity, T, X, ctrl, grad, w_cur, m_cur, v_cur);
+  }
 }
 
 }  // namespace swarm

@@ -108,7 +108,13 @@ class PeerExchange:
 
     @classmethod
     def connect(cls, group=None, device=None, timeout_us: int = 0) -> "PeerExchange":
-        """Collective over ``group`` (every rank calls it): allocate, exchange IPC handles, map."""
+        """Collective over ``group`` (every rank calls it): allocate, exchange IPC handles, map.
+
+        Never raises on one rank alone: a failure to allocate, to export the handle or to map a
+        peer's buffer is recorded in ``.error`` and the rank still enters every collective of the
+        setup (the handle gather and the barrier), so the ranks' collectives stay matched and
+        ``selftest()`` then fails on it without launching.  A world larger than
+        SWARM_PEER_MAX raises ValueError on every rank alike, before any collective."""
         import ctypes
         import torch.distributed as dist
         from . import _lib
@@ -117,15 +123,24 @@ class PeerExchange:
         if W > _lib.PEER_MAX:
             raise ValueError(f"peer all-reduce supports up to {_lib.PEER_MAX} ranks (one node), got {W}")
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        own = cls._alloc(lib)
-        h = (ctypes.c_char * _lib.PEER_HANDLE_BYTES)()
-        _lib.check(lib.swarm_peer_ipc_handle(ctypes.c_void_p(own), h), "swarm_peer_ipc_handle")
+        err, own, mine = None, None, None
+        try:
+            own = cls._alloc(lib)
+            h = (ctypes.c_char * _lib.PEER_HANDLE_BYTES)()
+            _lib.check(lib.swarm_peer_ipc_handle(ctypes.c_void_p(own), h), "swarm_peer_ipc_handle")
+            mine = bytes(h)
+        except RuntimeError as e:   # keep going: this rank still joins the gather and the barrier
+            err = e
         handles = [None] * W
-        dist.all_gather_object(handles, bytes(h), group=group)
-        recv, mapped, err = [], [], None
+        dist.all_gather_object(handles, mine, group=group)
+        recv, mapped = [], []
         for q, hq in enumerate(handles):
             if q == r:
                 recv.append(own)
+                continue
+            if hq is None:   # that rank has no buffer: its own error says why
+                err = err or RuntimeError(f"peer all-reduce: rank {q} could not set up its exchange buffer")
+                recv.append(None)
                 continue
             p = ctypes.c_void_p()
             buf = (ctypes.c_char * _lib.PEER_HANDLE_BYTES).from_buffer_copy(hq)
@@ -138,7 +153,7 @@ class PeerExchange:
             recv.append(int(p.value))
             mapped.append(int(p.value))
         dist.barrier(group)
-        end = cls(lib, W, r, own, [x or 0 for x in recv], dev, [own], mapped, timeout_us)
+        end = cls(lib, W, r, own or 0, [x or 0 for x in recv], dev, [own] if own else [], mapped, timeout_us)
         # a failed mapping does not raise here: this rank's buffer must stay allocated while the
         # others (who mapped it) still run their self-test; selftest() then reports the failure
         # on this rank without launching, and the others' waits expire on it (bench.py falls

@@ -150,14 +150,26 @@ class DQNTrainer:
         self.writer.add_scalar("Loss", c["loss"], c["tick"])
         return c["loss"]
 
-    def _episode_fn(self):
+    def _episode_fn(self, max_steps: int):
+        """One training tick plus the bookkeeping the reference does on the host every tick
+        (train_gcn_dqn.py:174-177), kept on the device: the episode's reward and loss sums, and
+        per tick the summed agent reward ('Reward', :174), the TD loss and whether an update
+        ran ('Loss' is logged only by updates, :113-115,136).  The tick's slot in the per-tick
+        buffers is fixed when the call is made, so a captured episode replays into the same
+        slots; train_model reads them once per episode."""
         eng = self.engine
         n = self.env.n_agents
+        calls = [0]
 
         def tick():
+            i = calls[0] % max_steps
+            calls[0] += 1
             eng.train_tick(full_out=False)
             self._acc_reward.add_(eng.reward[:, 0].mean() / n)
             self._acc_loss.add_(eng.ctrl.view(torch.float32)[5])
+            self._tick_reward[i].copy_(eng.reward.sum(dim=1).mean())
+            self._tick_loss[i].copy_(eng.ctrl.view(torch.float32)[5])
+            self._tick_trained[i].copy_(eng.ctrl[7])
         return tick
 
     def train_model(self, config):
@@ -170,7 +182,11 @@ class DQNTrainer:
         epsilon = initial_epsilon
         self._acc_reward = torch.zeros((), device=eng.device)
         self._acc_loss = torch.zeros((), device=eng.device)
-        tick_fn = self._episode_fn()
+        self._tick_reward = torch.zeros(max_steps, device=eng.device)
+        self._tick_loss = torch.zeros(max_steps, device=eng.device)
+        self._tick_trained = torch.zeros(max_steps, dtype=torch.int32, device=eng.device)
+        tick_fn = self._episode_fn(max_steps)
+        ticks = 0
         graph = None
         for episode in range(episodes):
             eng.reset()
@@ -187,6 +203,13 @@ class DQNTrainer:
             epsilon = max(min_epsilon, initial_epsilon * np.exp(-epsilon_decay * episode))
             average_loss = float(self._acc_loss.item()) / max_steps
             ep_reward = float(self._acc_reward.item())
+            # the per-tick scalars of the episode, read once (train_gcn_dqn.py:136,174)
+            rew_t, loss_t, tr_t = self._tick_reward.tolist(), self._tick_loss.tolist(), self._tick_trained.tolist()
+            for i in range(max_steps):
+                ticks += 1
+                self.writer.add_scalar("Reward", rew_t[i], ticks)
+                if tr_t[i]:
+                    self.writer.add_scalar("Loss", loss_t[i], ticks)
             eng.check_handoffs()   # an overrun hand-off dropped TD graphs: fail loudly (one 4-byte read)
             if eng.peer is not None:
                 eng.peer.check()   # an expired peer-exchange wait: the summed gradient is wrong

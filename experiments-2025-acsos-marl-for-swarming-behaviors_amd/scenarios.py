@@ -87,7 +87,7 @@ class GoToPositionScenario(BaseScenario):
 class ObstacleAvoidanceScenario(BaseScenario):
     """obstacle_avoidance_scenario.py: obstacle (-0.1, 0.1) r=0.05, reward
     -d_goal + 2.5 * (d_obs <= 1 ? -(1 - d_obs) : 0), hits = #[d_obs <= 0.2];
-    reset centre (0.6,-0.6) + (random ? N(0, 0.1) : 0) (:242-281)."""
+    reset centre (0.6,-0.6) + (random ? N(0, 0.1) : 0) (:94-133; the centre :100-102)."""
 
     SCENARIO_ID = _lib.SWARM_OBSTACLE_AVOIDANCE
 

@@ -62,7 +62,7 @@ typedef struct swarm_config {
 } swarm_config;
 
 #define SWARM_F_SHARED_RESET 1   /* one reset centre for all envs (go_to_position_scenario.py:88) */
-#define SWARM_F_RANDOM_OA 2      /* ObstacleAvoidance random=True (obstacle_avoidance_scenario.py:248) */
+#define SWARM_F_RANDOM_OA 2      /* ObstacleAvoidance random=True (obstacle_avoidance_scenario.py:100) */
 
 /* Device-resident control block; kernels read and advance it so that a tick
  * sequence can be replayed from a captured hipGraph.  Layout is ABI. */
@@ -86,7 +86,11 @@ typedef struct swarm_ctrl {
   uint32_t sample_tick;   /* `sample_n` graphs, prepared by swarm_reduce_advance (words 16-22); */
   uint32_t sample_n;      /* recomputed from (tick, n) whenever the tags do not match          */
   uint32_t sample_bits;
-  uint32_t pad1[9];
+  uint32_t peer_hold;     /* word 23, sticky: 1 once a peer-exchange wait of swarm_reduce_advance_peer
+                             expired on this rank; every later optimizer step is then skipped (the
+                             summed gradient is wrong), so a timeout never reaches the weights.
+                             Cleared only by swarm_ctrl_init; PeerExchange.check() raises on it. */
+  uint32_t pad1[8];
 } swarm_ctrl;           /* 32 words */
 /* A fresh control block comes from swarm_ctrl_init (all counters 0, beta powers 1). */
 
@@ -239,7 +243,9 @@ int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
  * rank computes bitwise the same sum.  Tags come from per-block launch counters (`seq`, device
  * words zeroed once at setup; every rank must issue the same sequence of peer calls) and the
  * buffer is double-buffered by their parity, so nothing is ever reset.  Waits are bounded in
- * time: one that expires adds 1 to *err (the sum is then wrong: check err and fail loudly). */
+ * time: one that expires adds 1 to *err (the sum is then wrong: check err and fail loudly); in
+ * swarm_reduce_advance_peer it also sets ctrl->peer_hold, which stops every later optimizer step
+ * of this rank before it can apply the wrong sum. */
 #define SWARM_PEER_MAX 8
 #define SWARM_PEER_HANDLE_BYTES 64   /* hipIpcMemHandle_t */
 #define SWARM_PEER_SEQ_WORDS 256     /* launch counters per rank (device uint32, zeroed at setup) */

@@ -102,3 +102,31 @@ def reference_shaped_train(flat_params, scenario, N, seconds=10.0, eps=0.05, see
         ticks += 1
     dt = time.perf_counter() - t0
     return dict(agent_steps_per_s=ticks * N / dt, ticks=ticks, seconds=dt)
+
+
+def reference_shaped_eval(flat_params, scenario, N, k=5, seconds=5.0, max_steps=50, seed=0):
+    """BASELINE.json configs[0] (C1): the reference's evaluation script shape
+    (tests/test_go_to_position.py -> Simulator.run_simulation, simulator.py:47-109) at B = 1:
+    per tick a dict of observations, the kNN edge list rebuilt with torch.topk per agent
+    (simulator.py:9-26), the edge-list GAT forward under no_grad, argmax, the env step and the
+    scenario metrics; episodes of ``max_steps`` ticks from the reset grid."""
+    params = O.unflatten_params(flat_params)
+    ticks = 0
+    t0 = time.perf_counter()
+    episode = 0
+    while time.perf_counter() - t0 < seconds:
+        pos, vel = _init_state(scenario, 1, N, seed + episode)
+        for _ in range(max_steps):
+            obs = {f"agent{i}": torch.cat([pos[:, i], vel[:, i], O.f32(O.GOAL)[None]], -1) for i in range(N)}
+            x = torch.cat([torch.stack([obs[f"agent{i}"] for i in range(N)], 0).squeeze(1),
+                           torch.arange(N).float().unsqueeze(1)], 1)
+            ei = O.knn_edge_index(x[:, :2], k)
+            with torch.no_grad():
+                acts = torch.argmax(O.q_forward_edges(params, x, ei), dim=1)
+            st = O.env_step(pos, vel, acts[None], scenario)
+            _ = float(st["avg_dist"][0]), float(st["hits"][0])   # the per-tick metrics the Simulator records
+            pos, vel = st["pos"], st["vel"]
+            ticks += 1
+        episode += 1
+    dt = time.perf_counter() - t0
+    return dict(agent_steps_per_s=ticks * N / dt, ticks=ticks, seconds=dt)

@@ -46,8 +46,8 @@ from . import philox
 # ---------------------------------------------------------------------------
 # constants
 # ---------------------------------------------------------------------------
-GOAL = (-0.8, 0.8)              # go_to_position_scenario.py:86, obstacle_avoidance_scenario.py:245
-OBSTACLE = (-0.1, 0.1)          # obstacle_avoidance_scenario.py:247
+GOAL = (-0.8, 0.8)              # go_to_position_scenario.py:86, obstacle_avoidance_scenario.py:97
+OBSTACLE = (-0.1, 0.1)          # obstacle_avoidance_scenario.py:99
 SPHERE_RADIUS = 0.05            # VMAS Sphere() default radius (agents and the obstacle)
 COLLISION_FORCE = 100.0         # VMAS World collision_force default
 CONTACT_MARGIN = 1e-3           # VMAS World contact_margin default
@@ -181,9 +181,9 @@ def env_step(pos: torch.Tensor, vel: torch.Tensor, actions: torch.Tensor, scenar
         hits = torch.zeros(B)
     else:
         d_obs = (vector_norm2(pos_new - obst) - SPHERE_RADIUS) - SPHERE_RADIUS   # World.get_distance
-        obst_rew = torch.where(d_obs <= 1, -(1 - d_obs), torch.tensor(0.0))      # obstacle_avoidance_scenario.py:294-300
+        obst_rew = torch.where(d_obs <= 1, -(1 - d_obs), torch.tensor(0.0))      # obstacle_avoidance_scenario.py:146-152
         rew = -dist_goal + 2.5 * obst_rew
-        hits = (d_obs <= 0.2).sum(dim=1).to(torch.float32)                       # :318-321
+        hits = (d_obs <= 0.2).sum(dim=1).to(torch.float32)                       # obstacle_avoidance_scenario.py:170-173
     avg_dist = torch.mean(dist_goal, dim=1)
     out = dict(pos=pos_new, vel=vel_new, force=force, rew=rew, dist_goal=dist_goal,
                avg_dist=avg_dist, hits=hits, d_obs=d_obs)
@@ -690,24 +690,26 @@ def complete_batch_edge_index(S: int, N: int) -> torch.Tensor:
 
 
 def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma=0.99,
-                 edge_index=None, edge_index_next=None, conv: str = "gat"):
+                 edge_index=None, edge_index_next=None, conv: str = "gat", dtype=torch.float32):
     """TD loss and its gradient (train_gcn_dqn.py:113-124) on S sampled graphs of N nodes.
 
     s_state / s_next_state: [S,N,4] (pos, vel); actions [S,N] int; rewards [S,N].
     conv="gcn": the a13 GCNConv variant (parity unpinned) on complete graphs.
+    dtype=torch.float64 evaluates the same restatement in double precision from the same fp32
+    inputs: the "exact" value both fp32 paths (this oracle and the GPU) are measured against.
     Returns (loss, flat grad [N_PARAMS], online Q at the taken actions, TD targets).
     """
     if conv == "gcn":
         return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma)
     S, N, _ = s_state.shape
-    params = {k: v.clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
-    tparams = unflatten_params(flat_target)
-    x = node_features(s_state[..., :2], s_state[..., 2:4]).reshape(S * N, N_FEATURES)
-    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4]).reshape(S * N, N_FEATURES)
+    params = {k: v.to(dtype).clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
+    tparams = {k: v.to(dtype) for k, v in unflatten_params(flat_target).items()}
+    x = node_features(s_state[..., :2], s_state[..., 2:4]).reshape(S * N, N_FEATURES).to(dtype)
+    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4]).reshape(S * N, N_FEATURES).to(dtype)
     ei = complete_batch_edge_index(S, N) if edge_index is None else edge_index
     ein = ei if edge_index_next is None else edge_index_next
     a = actions.reshape(-1).to(torch.long)
-    r = rewards.reshape(-1).to(torch.float32)
+    r = rewards.reshape(-1).to(torch.float32).to(dtype)
     values = q_forward_edges(params, x, ei).gather(1, a.unsqueeze(1))
     with torch.no_grad():
         next_values = q_forward_edges(tparams, xn, ein).max(dim=1)[0]

@@ -26,6 +26,9 @@ def test_struct_layouts_match_the_header(tmp_path):
         for field, _ in cls._fields_:
             lines.append(f'  printf("{name}.{field} %zu\\n", offsetof({name}, {field}));')
     lines.append('  printf("swarm_ctrl size %zu\\n", sizeof(swarm_ctrl));')
+    import swarm_amd._lib as L
+    for field in L.CTRL:
+        lines.append(f'  printf("swarm_ctrl.{field} %zu\\n", offsetof(swarm_ctrl, {field}));')
     lines.append("  return 0;\n}")
     src = tmp_path / "layout.c"
     src.write_text("\n".join(lines))
@@ -39,3 +42,5 @@ def test_struct_layouts_match_the_header(tmp_path):
             assert int(got[f"{name}.{field}"]) == getattr(cls, field).offset, f"{name}.{field}"
     import swarm_amd._lib as L
     assert int(got["swarm_ctrl size"]) == 4 * L.CTRL_WORDS
+    for field, word in L.CTRL.items():   # the word indices the host reads ctrl by
+        assert int(got[f"swarm_ctrl.{field}"]) == 4 * word, field

@@ -90,3 +90,68 @@ def test_allreduce_equals_union_batch(tmp_path):
     np.testing.assert_allclose(res[0]["norm"], ref["total_norm"], rtol=1e-5)
     np.testing.assert_allclose(res[0]["params"].numpy(), ref["params"].numpy(), rtol=0, atol=2e-6)
     np.testing.assert_allclose(res[0]["m"].numpy(), ref["m"].numpy(), rtol=1e-4, atol=1e-9)
+
+
+class _FakePeerLib:
+    """Host-side stand-in for libswarm_hip's peer setup calls (no GPU here): buffers are fake
+    addresses, handles carry the owner's rank; ``fail`` makes this rank's allocation fail.
+    It refuses any launch: a rank whose setup failed must never start an exchange."""
+
+    def __init__(self, rank, fail):
+        self.rank, self.fail = rank, fail
+
+    def swarm_peer_alloc(self, pp):
+        if self.fail:
+            return 2   # hipErrorOutOfMemory
+        pp._obj.value = 0x1000 * (self.rank + 1)
+        return 0
+
+    def swarm_peer_ipc_handle(self, buf, h):
+        import ctypes
+        ctypes.memmove(h, bytes([self.rank + 1]) * len(h), len(h))
+        return 0
+
+    def swarm_peer_ipc_open(self, buf, pp):
+        pp._obj.value = 0x100000 + bytes(buf)[0]
+        return 0
+
+    def swarm_peer_ipc_close(self, p):
+        return 0
+
+    def swarm_peer_free(self, p):
+        return 0
+
+    def swarm_peer_allreduce(self, *a):
+        raise AssertionError("an exchange was launched after a failed setup")
+
+
+def _peer_setup_main(rank, port, out_path, fail_rank):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    torch.set_num_threads(1)
+    import swarm_amd._lib as L
+    L.load = lambda *a, **k: _FakePeerLib(rank, rank == fail_rank)
+    pg = swdist.init_process_group("gloo")
+    end = swdist.PeerExchange.connect(pg, device="cpu")
+    ok = end.selftest()
+    # bench.py's decision: a MIN all-reduce of the flags, the same on every rank
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    end.close()
+    torch.save(dict(ok=ok, error=str(end.error), flag=int(flag.item())), f"{out_path}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_peer_setup_failure_on_one_rank_keeps_collectives_matched(tmp_path, fail_rank):
+    """one rank's swarm_peer_alloc fails.  Both ranks still complete connect() (the
+    handle gather and the barrier are always entered), neither launches an exchange, and the
+    MIN of the self-test flags is 0 on both: bench.py falls back to RCCL on every rank together
+    instead of hanging in mismatched collectives."""
+    out = str(tmp_path / "rank")
+    mp.start_processes(_peer_setup_main, args=(_free_port(), out, fail_rank), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(WORLD)]
+    assert all(not x["ok"] and x["flag"] == 0 for x in res)
+    assert "swarm_peer_alloc" in res[fail_rank]["error"]
+    assert f"rank {fail_rank} could not set up" in res[1 - fail_rank]["error"]

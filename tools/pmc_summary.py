@@ -25,7 +25,7 @@ def main(src, dst):
             for key, pat in KERNELS.items():
                 if pat in r["Kernel_Name"]:
                     vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    out = {"source": "rocprofv3 --kernel-trace --pmc, four separate passes (scripts/pmc.sh), bench.py workload",
+    out = {"source": "rocprofv3 --kernel-trace --pmc, separate passes (scripts/pmc.sh), bench.py workload",
            "units": "counter medians per dispatch; *_bytes in bytes",
            "kernels": {}}
     for key in KERNELS:
@@ -43,6 +43,10 @@ def main(src, dst):
             "per_wave": {c: k[c] / waves for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA",
                                                     "SQ_WAVE_CYCLES", "SQ_WAIT_ANY") if c in k},
         }
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in k and k.get("GRBM_GUI_ACTIVE"):
+            # MFMA pipe cycles over every SIMD's cycles while the GPU was busy with the dispatch:
+            # GRBM_GUI_ACTIVE sums the 8 XCDs, each with 128 SIMDs (reads high on short dispatches)
+            out["kernels"][key]["mfma_busy_frac_grbm"] = k["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * k["GRBM_GUI_ACTIVE"])
     main_k = "tick" if "tick" in out["kernels"] else "td"   # the bench line's dominant kernel
     if main_k in out["kernels"]:
         out["kernel"] = main_k
