@@ -476,7 +476,13 @@ def cpu_baseline_leg(args, w0, scen, B, N, S, eng):
     usable = info["affinity"]
     if info["cgroup_quota_cpus"]:
         usable = max(1, min(usable, math.ceil(info["cgroup_quota_cpus"])))
-    counts = sorted({usable, info["os_cpu_count"]})
+    # os.cpu_count() threads as well, unless a cgroup quota caps the process below that: there a
+    # 256-thread oracle on a 16-CPU quota ran 1 tick in 18.6 s (profiles/r03_v1_bench.json),
+    # oversubscription, not a baseline
+    quota_capped = info["cgroup_quota_cpus"] is not None and info["cgroup_quota_cpus"] < info["os_cpu_count"]
+    counts = [usable] if quota_capped else sorted({usable, info["os_cpu_count"]})
+    info["threads_rule"] = ("the cgroup CPU quota (all the CPU time this process may use)" if quota_capped else
+                            "the CPUs this process may run on, and os.cpu_count()")
     sid = 0 if scen == "GoTo" else 1
     sweep = []
     for th in counts:

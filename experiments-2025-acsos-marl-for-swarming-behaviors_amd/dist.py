@@ -96,6 +96,7 @@ class PeerExchange:
             arr[q] = p
         self.struct = SwarmPeer(world_size, rank, arr, self.seq.data_ptr(), self.err.data_ptr(), int(timeout_us), 0)
         self.error = None   # connect(): the first failed IPC mapping, if any
+        self._stream = None  # the one stream this rank's peer launches are ordered on (check_stream)
 
     # ------------------------------------------------------------------ construction
     @staticmethod
@@ -173,11 +174,29 @@ class PeerExchange:
         return ends
 
     # ------------------------------------------------------------------ use
+    def check_stream(self):
+        """The exchange's double-buffer argument (swarm_peer.h: parity s & 1 is safe because a
+        rank's launch s + 2 follows its launch s in STREAM ORDER) holds only if every peer
+        launch of this rank is ordered on one stream.  The first eager launch binds that stream;
+        an eager launch from another stream raises.  Launches recorded into a hipGraph are not
+        checked here: replay the graph on the bound stream (SwarmEngine and bench.py do)."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if self._stream is None:
+            self._stream = cur
+        elif cur != self._stream:
+            raise RuntimeError("peer all-reduce: every peer launch of a rank must be on one stream (the first "
+                               f"eager launch used {self._stream}, this one {cur}); unordered launches could reuse "
+                               "a parity slot of the exchange buffer before the other ranks read it")
+
     def allreduce_(self, x: torch.Tensor) -> torch.Tensor:
-        """In-place rank-ordered SUM of a flat fp32 device tensor (<= 1,674 elements)."""
+        """In-place rank-ordered SUM of a flat fp32 device tensor (<= 1,674 elements), launched on
+        the current stream, which must be this rank's one peer stream (``check_stream``)."""
         from ._lib import check, stream_ptr
         import ctypes
         assert x.is_contiguous() and x.dtype == torch.float32 and x.device == self.device
+        self.check_stream()
         check(self.lib.swarm_peer_allreduce(ctypes.byref(self.struct), x.data_ptr(), x.numel(), stream_ptr()),
               "swarm_peer_allreduce")
         return x
@@ -200,11 +219,13 @@ class PeerExchange:
         if self.error is not None:
             return False
         n = N_PARAMS + 1
-        col = torch.arange(n, dtype=torch.float32, device=self.device)
-        x = (self.rank + 1) * (1 + col)
-        self.allreduce_(x)
-        want = (self.world_size * (self.world_size + 1) / 2) * (1 + col)
-        ok = bool(torch.equal(x, want)) and self.errors() == 0
+        st = self._stream if self._stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(st):   # on this rank's peer stream (check_stream)
+            col = torch.arange(n, dtype=torch.float32, device=self.device)
+            x = (self.rank + 1) * (1 + col)
+            self.allreduce_(x)
+            want = (self.world_size * (self.world_size + 1) / 2) * (1 + col)
+            ok = bool(torch.equal(x, want)) and self.errors() == 0
         return ok
 
     def close(self):

@@ -317,6 +317,7 @@ class SwarmEngine:
     def launch_reduce_advance(self):
         """Slab reduce + ctrl advance; with a peer exchange, the gradient all-reduce too."""
         if self.peer is not None:
+            self.peer.check_stream()
             check(self.lib.swarm_reduce_advance_peer(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
                                                      ctypes_ref(self.learner), self.capacity, ptr(self.ctrl),
                                                      ctypes_ref(self.peer.struct), stream_ptr()),

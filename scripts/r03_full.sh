@@ -1,0 +1,15 @@
+#!/bin/bash
+# full GPU suite (achieved errors to gpurun_out/parity_errors.json), smoke, the TD-delay A/B, the
+# default bench line.  Stops at the first failure.
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED" gpurun_out/pytest_gpu.log | head -30; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+if [ -n "$VARIANTS" ]; then bash scripts/ab_bench.sh || exit $?; fi
+timeout -k 10 600 python bench.py > gpurun_out/bench_default.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_default.log
+exit $rc

@@ -3,7 +3,7 @@
 # recorded data (tools/train_parity.py, tools/eval_sweep.py).
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 800 python -u tools/train_parity.py gpurun_out/train_parity.json > gpurun_out/train_parity.log 2>&1
+timeout -k 10 800 python -u tools/train_parity.py --out gpurun_out/train_parity.json --agents 5,10 > gpurun_out/train_parity.log 2>&1
 rc=$?; cat gpurun_out/train_parity.log | tail -12
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -u tools/eval_sweep.py /tmp/eval_sweep > gpurun_out/eval_sweep.log 2>&1

@@ -47,6 +47,8 @@ def rank_streams(sw):
             ss = [torch.cuda.Stream(priority=-1) for _ in range(3)]
             x = [torch.ones(16, device="cuda") for _ in range(3)]
             before = [e.errors() for e in probe]
+            for e in probe:
+                e._stream = None   # each attempt binds its own candidate streams
             for r, s in enumerate(ss):
                 with torch.cuda.stream(s):
                     probe[r].allreduce_(x[r])
@@ -74,7 +76,8 @@ def _on_streams(streams, ends, fn):
 
 # in one process every emulated rank needs a hardware queue of its own (its kernels wait on the
 # others'): the box gives a process GPU_MAX_HW_QUEUES = 4, one of them torch's current stream.
-# More ranks run as processes (test_two_process_ipc_exchange, W = 8).
+# More ranks run as processes: test_two_process_ipc_exchange (the fused tick, W = 2, 3) and
+# test_eight_process_standalone_allreduce (the standalone exchange, W = 8).
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_peer_allreduce_sums_in_rank_order(sw, rank_streams, world):
     from swarm_amd.dist import PeerExchange
@@ -97,6 +100,23 @@ def test_peer_allreduce_sums_in_rank_order(sw, rank_streams, world):
         ends[0].close()
 
 
+def test_peer_launches_must_share_one_stream(sw):
+    """the parity double buffer is safe only for stream-ordered launches, so an eager
+    peer launch from a second stream raises instead of reusing a slot silently."""
+    from swarm_amd.dist import PeerExchange
+    (end,) = PeerExchange.local(1)
+    try:
+        x = torch.ones(16, device="cuda")
+        end.allreduce_(x)
+        with torch.cuda.stream(torch.cuda.Stream()):
+            with pytest.raises(RuntimeError, match="one stream"):
+                end.allreduce_(x)
+        torch.cuda.synchronize()
+        assert end.selftest()   # runs on the bound stream
+    finally:
+        end.close()
+
+
 def test_peer_wait_expires_and_is_counted(sw):
     """Only rank 0 of two launches: its waits for rank 1 expire (short bound), are counted, and
     check() fails loudly."""
@@ -110,6 +130,37 @@ def test_peer_wait_expires_and_is_counted(sw):
         with pytest.raises(RuntimeError, match="peer all-reduce"):
             ends[0].check()
         assert ends[1].errors() == 0
+    finally:
+        ends[0].close()
+
+
+def test_expired_exchange_never_reaches_the_weights(sw, golden_weights):
+    """rank 0 of two trains alone, so every exchange wait of its fused reduce expires
+    (2 ms bound).  The reduce sets the sticky ctrl.peer_hold; the next ticks' in-register optimizer
+    steps and the flush then apply nothing: the weights, moments and Adam step stay as they were
+    instead of absorbing the wrong sum, and check() raises."""
+    from swarm_amd.dist import PeerExchange
+    from swarm_amd._lib import CTRL
+    p = _params(golden_weights)
+    ends = PeerExchange.local(2, timeout_us=2000)
+    try:
+        eng = sw.SwarmEngine("GoTo", 8, 32, seed=5, params=p, batch=32, replay_capacity=32 * 4, eps=0.2,
+                             world_size=2, peer=ends[0])
+        eng.reset(0)
+        for _ in range(2):
+            eng.act(push=True, full_out=False)
+            eng.advance()
+        w0, m0 = eng.params.clone(), eng.adam_m.clone()
+        for _ in range(3):
+            eng.train_tick()
+        eng.flush()
+        torch.cuda.synchronize()
+        assert ends[0].errors() > 0
+        assert int(eng.ctrl[CTRL["peer_hold"]].item()) == 1
+        assert torch.equal(eng.params, w0) and torch.equal(eng.adam_m, m0)
+        assert eng.read_ctrl()["adam_step"] == 0
+        with pytest.raises(RuntimeError, match="peer all-reduce"):
+            ends[0].check()
     finally:
         ends[0].close()
 
@@ -256,3 +307,45 @@ def test_two_process_ipc_exchange(sw, golden_weights, tmp_path, world):
     for r in res[1:]:
         assert torch.equal(res[0]["params"], r["params"]) and torch.equal(res[0]["v"], r["v"])
     assert res[0]["ctrl"]["tick"] == 21 and res[0]["ctrl"]["adam_step"] >= 19
+
+
+def _allreduce8_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from swarm_amd.dist import PeerExchange
+    peer = PeerExchange.connect(dist.group.WORLD, timeout_us=3_000_000)   # a stuck wait fails in 3 s
+    ok = peer.selftest()
+    res = []
+    # several launches per size: tags 1..k and both parities of every column block's slot; the
+    # inputs are fp32 values whose sum depends on the order, so bitwise equality with the
+    # rank-ordered sum checks the order too
+    for k, n in enumerate([1674, 1674, 17, 1, 1674, 333, 1674]):
+        xs = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * k + q)) * (q + 1) for q in range(world)]
+        want = xs[0].clone()
+        for q in range(1, world):
+            want = want + xs[q]
+        x = xs[rank].cuda()
+        dist.barrier()
+        peer.allreduce_(x)
+        torch.cuda.synchronize()
+        res.append(bool(torch.equal(x.cpu(), want)))
+    torch.save({"ok": ok, "errors": peer.errors(), "res": res}, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    peer.close()
+    dist.destroy_process_group()
+
+
+def test_eight_process_standalone_allreduce(sw, tmp_path):
+    """the W = 8 exchange (SWARM_PEER_MAX) executed.  Eight processes share the one
+    GPU, HIP IPC handles over a gloo group, and run the standalone swarm_peer_allreduce (one
+    128-thread block per 16 columns and rank: 8 x 105 blocks, all resident at once): the
+    setup self-test, then seven all-reduces of 1 to 1,674 columns (tags 1-8 per column block,
+    both parities), each bitwise equal to the rank-ordered fp32 sum on every rank."""
+    import torch.multiprocessing as mp
+    world = 8
+    mp.spawn(_allreduce8_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    assert all(r["ok"] and r["errors"] == 0 for r in res), [(r["ok"], r["errors"]) for r in res]
+    assert all(all(r["res"]) for r in res), [r["res"] for r in res]
