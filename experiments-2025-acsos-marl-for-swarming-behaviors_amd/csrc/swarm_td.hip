@@ -52,6 +52,19 @@ struct ReduceArgs {
 #ifndef SWARM_RED_GROUPS
 #define SWARM_RED_GROUPS 64
 #endif
+// The ping-pong copy-back (w / m / v _nxt -> _cur) runs in three extra blocks of its own (one
+// array each, a float4 per thread) beside the column blocks (1); 0 = in waves 0-2 of every column
+// block after its slab loads (round 2).  14.24 -> 14.09 us per tick, three interleaved pairs
+// (profiles/r03_ab_reduce.jsonl)
+#ifndef SWARM_RED_COPY_BLOCKS
+#define SWARM_RED_COPY_BLOCKS 1
+#endif
+constexpr int kRedCopyBlocks = SWARM_RED_COPY_BLOCKS ? 3 : 0;
+// A/B knob: 1 = the 64 group sums of a column combined by permlane swaps within each wave, then
+// the 16 wave sums (one barrier); 0 = two LDS levels (8 runs of 8, then the runs; two barriers)
+#ifndef SWARM_RED_DPP
+#define SWARM_RED_DPP 0
+#endif
 constexpr int kRedCols = SWARM_RED_COLS;
 constexpr int kRedGroups = SWARM_RED_GROUPS;
 constexpr int kRedRuns = kRedGroups / 8;   // first combine level: runs of 8 group sums
@@ -71,6 +84,13 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
   swarm_ctrl* C = ctrl;
+  if (kRedCopyBlocks && (int)blockIdx.x > kRedColBlocks) {   // advance mode: a copy-back block
+    const int j = (int)blockIdx.x - kRedColBlocks - 1;
+    const float4* src = reinterpret_cast<const float4*>(j == 0 ? A.lr.w_nxt : (j == 1 ? A.lr.m_nxt : A.lr.v_nxt));
+    float4* dst = reinterpret_cast<float4*>(j == 0 ? A.lr.w_cur : (j == 1 ? A.lr.m_cur : A.lr.v_cur));
+    if ((int)threadIdx.x < N_PARAMS_PAD / 4) dst[threadIdx.x] = src[threadIdx.x];
+    return;
+  }
   if ((int)blockIdx.x == kRedColBlocks) {   // advance mode: the control block
     // thread 0 advances the counters and the Adam scalars; thread 64 (another wave) derives
     // the next tick's sampling key; both read ctrl before the barrier, write after it
@@ -145,12 +165,27 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
       for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }
   }
-  if (advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
+  if (!kRedCopyBlocks && advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
     if (q == 0) A.lr.w_cur[col] = A.lr.w_nxt[col];
     else if (q == 1) A.lr.m_cur[col] = A.lr.m_nxt[col];
     else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
   }
   SWARM_STAMP(29);
+#if SWARM_RED_DPP
+  // the four groups of a wave (lanes c, c + 16, c + 32, c + 48) combined by permlane swaps, then
+  // the kRedGroups / 4 wave sums of a column in wave order: one block barrier
+  static_assert(kRedCols == 16, "one column per lane of a 16-lane row");
+  {
+    const float ws = row4_sum(s);
+    if ((threadIdx.x & 63) < kRedCols) part[threadIdx.x >> 6][c] = ws;
+  }
+  __syncthreads();
+  SWARM_STAMP(30);
+  if (q == 0 && col <= N_PARAMS) {
+    float tot = part[0][c];
+#pragma unroll
+    for (int gi = 1; gi < kRedGroups / 4; ++gi) tot = tot + part[gi][c];
+#else
   part[q][c] = s;
   __syncthreads();
   SWARM_STAMP(30);
@@ -165,6 +200,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     float tot = part2[0][c];
 #pragma unroll
     for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
+#endif
     if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
     else A.grad[col] = tot;
     // this rank's loss of the update (0 when skipped: the TD launch wrote zero slabs)
@@ -357,10 +393,10 @@ static int reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, con
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
   if (peer)
-    hipLaunchKernelGGL(grad_reduce_kernel<1>, dim3(kRedColBlocks + 1), dim3(kRedCols * kRedGroups), 0,
+    hipLaunchKernelGGL(grad_reduce_kernel<1>, dim3(kRedColBlocks + 1 + kRedCopyBlocks), dim3(kRedCols * kRedGroups), 0,
                        (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   else
-    hipLaunchKernelGGL(grad_reduce_kernel<0>, dim3(kRedColBlocks + 1), dim3(kRedCols * kRedGroups), 0,
+    hipLaunchKernelGGL(grad_reduce_kernel<0>, dim3(kRedColBlocks + 1 + kRedCopyBlocks), dim3(kRedCols * kRedGroups), 0,
                        (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }

@@ -120,6 +120,15 @@ struct TdFused {
 #ifndef SWARM_HO_FORCE_DROP
 #define SWARM_HO_FORCE_DROP 0
 #endif
+#ifndef SWARM_HO_PIPE
+#define SWARM_HO_PIPE 0   // A/B: two hand-off sweeps in flight (tools/ab_build.py); slower (r03)
+#endif
+#ifndef SWARM_HO_SLEEP
+#define SWARM_HO_SLEEP 1  // s_sleep argument (x 64 cycles) between two hand-off sweeps
+#endif
+#ifndef SWARM_HO_PREPOLL
+#define SWARM_HO_PREPOLL 0   // A/B: poll one granule per lane until it matches, then sweep all five
+#endif
 constexpr int kHoSpinLimit = SWARM_HO_SPIN_LIMIT;   // polls (with s_sleep) before a hand-off wait gives up
 // test builds only (libswarm_hip_hodrop.so): every hand-off wait overruns at once
 constexpr bool kHoForceDrop = SWARM_HO_FORCE_DROP != 0;
@@ -290,35 +299,89 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off):
                     // online waves s and a, target waves s' (r is swept before y)
       const uint32_t tag = cc.tick + 1u;
-      for (int spin = 0;; ++spin) {
-        bool ok = true;
-        bool okc[CT];
+      // one sweep: this lane's 5 granules of every hand-off graph slot (ct)
+      struct Sweep { unsigned long long g[CT][5]; };
+      auto issue = [&](Sweep& w) {
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          okc[ct] = true;
           if (ho[ct]) {
             const unsigned long long* rec = ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
             const int j = min(jl[ct], N - 1);
             const unsigned long long* sp = rec + (online ? 0 : 4 * N) + 4 * j;
-            const unsigned long long g0 = ld_granule(sp), g1 = ld_granule(sp + 1), g2 = ld_granule(sp + 2),
-                                     g3 = ld_granule(sp + 3);
-            const unsigned long long g4 = online ? ld_granule(rec + 9 * N + j) : ((unsigned long long)tag << 32);
-            okc[ct] = !kHoForceDrop && (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag &&
-                      (uint32_t)(g2 >> 32) == tag && (uint32_t)(g3 >> 32) == tag && (uint32_t)(g4 >> 32) == tag;
-            ok = ok && okc[ct];
-            st[ct] = make_float4(__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1),
-                                 __uint_as_float((uint32_t)g2), __uint_as_float((uint32_t)g3));
-            if (online) act[ct] = nv[ct] ? (int)(uint32_t)g4 : 0;
+            w.g[ct][0] = ld_granule(sp); w.g[ct][1] = ld_granule(sp + 1); w.g[ct][2] = ld_granule(sp + 2);
+            w.g[ct][3] = ld_granule(sp + 3);
+            w.g[ct][4] = online ? ld_granule(rec + 9 * N + j) : ((unsigned long long)tag << 32);
           }
         }
-        if (!__builtin_amdgcn_ballot_w64(!ok)) break;
+      };
+      // take a sweep's values; true when every tag of the wave matched
+      auto take = [&](const Sweep& w, bool (&okc)[CT]) -> bool {
+        bool ok = true;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          okc[ct] = true;
+          if (ho[ct]) {
+            okc[ct] = !kHoForceDrop && (uint32_t)(w.g[ct][0] >> 32) == tag && (uint32_t)(w.g[ct][1] >> 32) == tag &&
+                      (uint32_t)(w.g[ct][2] >> 32) == tag && (uint32_t)(w.g[ct][3] >> 32) == tag &&
+                      (uint32_t)(w.g[ct][4] >> 32) == tag;
+            ok = ok && okc[ct];
+            st[ct] = make_float4(__uint_as_float((uint32_t)w.g[ct][0]), __uint_as_float((uint32_t)w.g[ct][1]),
+                                 __uint_as_float((uint32_t)w.g[ct][2]), __uint_as_float((uint32_t)w.g[ct][3]));
+            if (online) act[ct] = nv[ct] ? (int)(uint32_t)w.g[ct][4] : 0;
+          }
+        }
+        return !__builtin_amdgcn_ballot_w64(!ok);
+      };
+#if SWARM_HO_PIPE
+      // two sweeps in flight: the next sweep's loads are issued before this one is checked, so a
+      // granule that lands between two sweeps is seen half a round trip sooner
+      Sweep sa, sb;
+      issue(sa);
+      for (int spin = 0;; spin += 2) {
+        bool okc[CT];
+        __builtin_amdgcn_s_sleep(1);
+        issue(sb);
+        if (take(sa, okc)) break;
         if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
           if (lane == 0) atomicAdd(X.ho_err, 1u);
           drop_overrun<NS, GS>(okc, live_drop, nv, c);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
+        issue(sa);
+        if (take(sb, okc)) break;
       }
+#else
+#if SWARM_HO_PREPOLL
+      // while the acting wave is still computing, poll only this lane's first granule of each
+      // hand-off slot (a fifth of the sweep's loads); the full sweep below then normally matches
+      // at once (the other four granules were stored beside it)
+      for (int spin = 0; spin < kHoSpinLimit; ++spin) {
+        bool ok = true;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          if (ho[ct]) {
+            const unsigned long long* rec = ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
+            const unsigned long long g0 = ld_granule(rec + (online ? 0 : 4 * N) + 4 * min(jl[ct], N - 1));
+            ok = ok && (uint32_t)(g0 >> 32) == tag;
+          }
+        if (kHoForceDrop || !__builtin_amdgcn_ballot_w64(!ok)) break;
+        __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
+      }
+#endif
+      for (int spin = 0;; ++spin) {
+        Sweep sw;
+        bool okc[CT];
+        issue(sw);
+        if (take(sw, okc)) break;
+        if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
+          if (lane == 0) atomicAdd(X.ho_err, 1u);
+          drop_overrun<NS, GS>(okc, live_drop, nv, c);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
+      }
+#endif
       SWARM_RTSTAMP(10);
       __builtin_amdgcn_s_setprio(3);
     }
