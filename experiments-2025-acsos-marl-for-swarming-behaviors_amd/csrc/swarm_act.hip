@@ -22,6 +22,22 @@ __global__ __launch_bounds__(64 * kActWPB) void act_kernel(const swarm_ctrl* __r
   act_body<NS, MODE, SCEN, SPEC, false, NET>(S, blockIdx.x, gridDim.x, ctrl, state, grad, w_cur, m_cur, v_cur, B, N, A);
 }
 
+// A/B knob: SWARM_ROLLOUT_WPE = w > 0 launches the multi-tick rollouts through this copy of the
+// kernel with an occupancy target of w waves per SIMD (the register budget the compiler may
+// use); 0 = act_kernel with the compiler's default
+#ifndef SWARM_ROLLOUT_WPE
+#define SWARM_ROLLOUT_WPE 0
+#endif
+#if SWARM_ROLLOUT_WPE > 0
+template <int NS, int MODE, int SCEN, int SPEC, int NET = SWARM_NET_GCN>
+__global__ __launch_bounds__(64 * kActWPB) __attribute__((amdgpu_waves_per_eu(SWARM_ROLLOUT_WPE, SWARM_ROLLOUT_WPE)))
+void act_kernel_w(const swarm_ctrl* __restrict__ ctrl, float* state, const float* grad, const float* w_cur,
+                  const float* m_cur, const float* v_cur, int B, int N, ActArgs A) {
+  __shared__ ActSmem<NS> S;
+  act_body<NS, MODE, SCEN, SPEC, false, NET>(S, blockIdx.x, gridDim.x, ctrl, state, grad, w_cur, m_cur, v_cur, B, N, A);
+}
+#endif
+
 // ---------------------------------------------------------------- reset
 // reset_world_at + generate_grid; centre from Philox + Box-Muller (fp32 libm)
 __global__ void reset_kernel(int B, int N, int scenario, int flags, uint32_t k0, uint32_t k1, int env_offset,
@@ -168,8 +184,18 @@ int launch_act(const ActArgs& a, int tiles, hipStream_t st) {
   constexpr int S3 = MODE == MODE_ROLLOUT ? SPEC_KNN_GAT : SPEC_RUNTIME;
   constexpr int S4 = MODE == MODE_ROLLOUT ? SPEC_RADIUS_GAT : SPEC_RUNTIME;   // GoTo, N <= 8 only
   const int spec = kTick ? spec_of(a.graph, a.conv) : SPEC_RUNTIME;
+#if SWARM_ROLLOUT_WPE > 0
+#define SWARM_ACT_LAUNCH1(NS, SC, SP)                                                                               \
+  do {                                                                                                              \
+    if constexpr (MODE == MODE_ROLLOUT)                                                                             \
+      hipLaunchKernelGGL((act_kernel_w<NS, MODE, SC, SP>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a); \
+    else                                                                                                            \
+      hipLaunchKernelGGL((act_kernel<NS, MODE, SC, SP>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a); \
+  } while (0)
+#else
 #define SWARM_ACT_LAUNCH1(NS, SC, SP) \
   hipLaunchKernelGGL((act_kernel<NS, MODE, SC, SP>), grid, block, 0, st, a.ctrl, a.state, g, w, m, v, a.B, a.N, a)
+#endif
 #define SWARM_ACT_LAUNCH(NS, SC)                                  \
   do {                                                            \
     if (spec == SPEC_COMPLETE_GAT) SWARM_ACT_LAUNCH1(NS, SC, S1);  \
@@ -335,6 +361,18 @@ int swarm_rollout(const swarm_config* cfg, const float* params, float* state, in
   return launch_act<MODE_ROLLOUT>(a, n_tiles(cfg), (hipStream_t)stream);
 }
 
+#if SWARM_DIAG_TIE_COUNT
+// diagnostic library only: {kNN builds (waves x ticks), builds with a tie row, tie rows} since load
+int swarm_dbg_tie_counts(unsigned long long* out3) {
+  hipError_t e = hipMemcpyFromSymbol(&out3[0], HIP_SYMBOL(g_swarm_knn_calls), 8);
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(&out3[1], HIP_SYMBOL(g_swarm_tie_calls), 8);
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(&out3[2], HIP_SYMBOL(g_swarm_tie_rows), 8);
+  return (int)e;
+}
+int swarm_dbg_tie_env(unsigned int* out4096) {
+  return (int)hipMemcpyFromSymbol(out4096, HIP_SYMBOL(g_swarm_tie_env), 4096 * 4);
+}
+#endif
 #if SWARM_STAMPS
 int swarm_dbg_stamps_act(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_swarm_stamps), &p, sizeof(p)); }
 #endif

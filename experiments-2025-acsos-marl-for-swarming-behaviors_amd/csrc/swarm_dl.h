@@ -169,9 +169,50 @@ __device__ inline int bit_sel_high(uint32_t m, int t) {
 // torch.topk on 60,000 tie-heavy rows (n 4..16) before it went in; the GPU tests compare the
 // sets with torch.topk (oracle knn_sets) and the recorded reference actions.
 // tb: ballot with bit n * lpn set for every tie row n; q: GS KV entries of LDS per slot.
+// A/B knobs: SWARM_TIE_NOINLINE = 1 keeps the (rarely taken) tie path out of line, so its
+// registers and code do not weigh on the caller; SWARM_DIAG_NO_TIE = 1 skips it (timing only:
+// wrong neighbour sets on tied rows, never shipped)
+#ifndef SWARM_TIE_NOINLINE
+#define SWARM_TIE_NOINLINE 0
+#endif
+#ifndef SWARM_DIAG_NO_TIE
+#define SWARM_DIAG_NO_TIE 0
+#endif
+#ifndef SWARM_TIE_FAST
+#define SWARM_TIE_FAST 0   // A/B: two lane hops per introselect round, group OR by DPP
+#endif
+#ifndef SWARM_DIAG_TIE_TWICE
+#define SWARM_DIAG_TIE_TWICE 0
+#endif
+#ifndef SWARM_DIAG_TIE_COUNT
+#define SWARM_DIAG_TIE_COUNT 0   // diagnostic builds: count tie-path entries (rows) and calls (waves)
+#endif
+#if SWARM_DIAG_TIE_COUNT
+__device__ unsigned long long g_swarm_tie_rows, g_swarm_tie_calls, g_swarm_knn_calls;
+__device__ unsigned int g_swarm_tie_env[4096];   // tie builds per acting wave (block * 4 + wave)
+#endif
+#ifndef SWARM_HEAP_NOINLINE
+#define SWARM_HEAP_NOINLINE 0   // A/B: the serial heap_select branch (depth limit) out of line
+#endif
+#ifndef SWARM_TIE_COLD
+#define SWARM_TIE_COLD 0        // A/B: the tie branch marked unlikely
+#endif
+#if SWARM_HEAP_NOINLINE
+static __device__ __attribute__((noinline)) void kv_heap_select_swap(KV* a, int first, int nth, int last) {
+#else
+static __device__ inline void kv_heap_select_swap(KV* a, int first, int nth, int last) {
+#endif
+  kv_heap_select(a, first, nth + 1, last);
+  kv_swap(a, first, nth);
+}
+#if SWARM_TIE_NOINLINE
+#define SWARM_TIE_INLINE __attribute__((noinline))
+#else
+#define SWARM_TIE_INLINE inline
+#endif
 template <int NS, int GS>
-__device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
-                                         const float* __restrict__ dn, KV* q) {
+__device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
+                                                   const float* __restrict__ dn, KV* q) {
   constexpr int G = GS <= 8 ? 8 : 16;   // lanes per row
   constexpr int NG = 64 / G;
   const int g = lane / G, e = lane % G, gb = lane - e;
@@ -192,6 +233,32 @@ __device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long l
       if (depth == 0) { heap = true; break; }
       --depth;
       const int mid = first + (last - first) / 2;
+#if SWARM_TIE_FAST
+      // two lane hops per round: the four values the round reads (the one at `first` too) in one
+      // hop; the median-of-3 swap applied locally (v1 = the array after it, pv = its pivot); the
+      // partition's permutation composed with that swap and applied to the ORIGINAL row in one
+      // hop (v'' = v[swap(part(e))])
+      const float v0 = __shfl(v, gb + first), vx = __shfl(v, gb + first + 1), vy = __shfl(v, gb + mid),
+                  vz = __shfl(v, gb + last - 1);
+      int pick;   // kv_move_median_to_first(first, first + 1, mid, last - 1)
+      if (vx < vy) pick = (vy < vz) ? mid : ((vx < vz) ? last - 1 : first + 1);
+      else if (vx < vz) pick = first + 1;
+      else pick = (vy < vz) ? last - 1 : mid;
+      const float pv = pick == mid ? vy : (pick == first + 1 ? vx : vz);   // moved to `first`
+      const float v1 = e == first ? pv : (e == pick ? v0 : v);
+      const uint32_t lm = gballot(e > first && e < last && !(v1 < pv));
+      const uint32_t rm = gballot(e >= first && e < last && !(pv < v1));
+      const bool is_l = (lm >> e) & 1u, is_r = (rm >> e) & 1u;
+      const int tl = __popc(lm & ((1u << e) - 1u)) + 1;   // rank among the left stoppers
+      const int above = __popc(rm >> (e + 1));             // right stoppers after e
+      const int T = __popc(gballot(is_l && above >= tl));
+      int src = e;
+      if (is_l && tl <= T) src = bit_sel_high(rm, tl);
+      if (is_r && above + 1 <= T) src = bit_sel_low(lm, above + 1);
+      src = src == first ? pick : (src == pick ? first : src);
+      v = __shfl(v, gb + src);
+      id = __shfl(id, gb + src);
+#else
       const float vx = __shfl(v, gb + first + 1), vy = __shfl(v, gb + mid), vz = __shfl(v, gb + last - 1);
       int pick;   // kv_move_median_to_first(first, first + 1, mid, last - 1)
       if (vx < vy) pick = (vy < vz) ? mid : ((vx < vz) ? last - 1 : first + 1);
@@ -212,6 +279,7 @@ __device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long l
       if (is_r && above + 1 <= T) src = bit_sel_low(lm, above + 1);
       v = __shfl(v, gb + src);
       id = __shfl(id, gb + src);
+#endif
       int cut = __ffs(lm) - 1;
       if (T > 0) {
         cut = bit_sel_high(rm, T);
@@ -224,10 +292,7 @@ __device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long l
       KV* a = q + n * GS;
       if (e < N) a[e] = KV{v, id};
       wave_lds_sync();
-      if (e == 0) {
-        kv_heap_select(a, first, nth + 1, last);
-        kv_swap(a, first, nth);
-      }
+      if (e == 0) kv_heap_select_swap(a, first, nth, last);
       wave_lds_sync();
       if (e < N) { v = a[e].v; id = a[e].i; }
     } else {      // kv_insertion_sort of [first, last), <= 3 elements: stable rank sort
@@ -246,8 +311,17 @@ __device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long l
       id = __shfl(id, gb + src);
     }
     uint32_t mm = e < k ? (1u << id) : 0u;
+#if SWARM_TIE_FAST
+    // OR over the group's lanes by DPP inside the 16-lane row (no lane hop): quad xor 1, quad
+    // xor 2, half-row mirror (lanes i <-> 7 - i), and for 16-lane groups the row mirror
+    mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0xB1, 0xF, 0xF, false);
+    mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0x4E, 0xF, 0xF, false);
+    mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0x141, 0xF, 0xF, false);
+    if (G == 16) mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0x140, 0xF, 0xF, false);
+#else
 #pragma unroll
     for (int s = G / 2; s >= 1; s >>= 1) mm |= (uint32_t)__shfl_xor((int)mm, s);
+#endif
     if (e == 0) sm.knn[n] = mm;
   }
 }
@@ -291,9 +365,24 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
   const bool tie = r == 0 && nvalid && __popc(mask) != k;
   if (r == 0) sm.knn[n] = nvalid ? mask : 0u;
   const unsigned long long tb = __ballot(tie);
-  if (tb) {   // boundary ties: the introselect restatement, G lanes per row
+#if SWARM_DIAG_TIE_COUNT
+  if (lane == 0) {
+    atomicAdd(&g_swarm_knn_calls, 1ull);
+    if (tb) {
+      atomicAdd(&g_swarm_tie_calls, 1ull);
+      atomicAdd(&g_swarm_tie_rows, (unsigned long long)__popcll(tb));
+      atomicAdd(&g_swarm_tie_env[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 4095], 1u);
+    }
+  }
+#endif
+  if (!SWARM_DIAG_NO_TIE && (SWARM_TIE_COLD ? __builtin_expect(tb != 0ull, 0) : tb != 0ull)) {
+    // boundary ties: the introselect restatement, G lanes per row
     wave_lds_sync();
     knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
+#if SWARM_DIAG_TIE_TWICE   // timing diagnostic: the same (idempotent) tie path a second time
+    wave_lds_sync();
+    knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
+#endif
   }
 }
 
