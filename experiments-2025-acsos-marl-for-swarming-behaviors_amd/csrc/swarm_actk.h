@@ -74,12 +74,25 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   float* red = S.red;
   SWARM_RTSTAMP(30);
   SWARM_STAMP(0);
+#if SWARM_STAMPS   // slot 29: where the wave runs (HW_ID in the low word, XCC_ID in the high word)
+  if (g_swarm_stamps && (threadIdx.x & 63) == 0)
+    g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + 29] =
+        (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+        ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
+#endif
   if (HO) __builtin_amdgcn_s_setprio(3);   // fused tick: acting waves ahead of the TD blocks beside them
   const int w = threadIdx.x >> 6;
   const DGeom<NS> d = make_dgeom<NS>(vb * kActWPB + w, B);
   const int graph = spec_graph<SPEC>(A.graph);
   const int conv = spec_conv<SPEC>(A.conv);
-  const WView<NS> V = SW[w].view();
+  // the kNN tie memo pays only across the ticks of one launch: rollouts
+  WView<NS> V = SW[w].view();
+  if constexpr (MODE == MODE_ROLLOUT) {
+    SW[w].memo.clear(threadIdx.x & 63);
+    wave_lds_sync();
+  } else {
+    V.memo = nullptr;
+  }
   WSmall<NS>& sm = SW[w].sm;
   const int c = d.c, p = d.p;
 
@@ -196,6 +209,9 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
 
   for (int it = 0; it < n_ticks; ++it) {
+#if SWARM_STAMPS   // stamps build: the wave's slowest tick (slot 25 cycles, slot 19 tick index)
+    const long long t_tick0 = clock64();
+#endif
     if (MODE != MODE_Q) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
@@ -422,6 +438,13 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       if (A.out.hits) A.out.hits[d.gid] = hits_sum;
     }
     wave_lds_sync();   // every lane done with this tick's LDS rows before the next tick rewrites them
+#if SWARM_STAMPS
+    if (g_swarm_stamps && (threadIdx.x & 63) == 0) {
+      unsigned long long* ws = g_swarm_stamps + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32;
+      const unsigned long long dt = (unsigned long long)(clock64() - t_tick0);
+      if (dt > ws[25]) { ws[25] = dt; ws[19] = (unsigned long long)it; }
+    }
+#endif
   }
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {

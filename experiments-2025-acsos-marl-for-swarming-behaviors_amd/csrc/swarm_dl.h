@@ -178,11 +178,11 @@ __device__ inline int bit_sel_high(uint32_t m, int t) {
 #ifndef SWARM_DIAG_NO_TIE
 #define SWARM_DIAG_NO_TIE 0
 #endif
-#ifndef SWARM_TIE_FAST
-#define SWARM_TIE_FAST 0   // A/B: two lane hops per introselect round, group OR by DPP
+#ifndef SWARM_TIE_LEGACY
+#define SWARM_TIE_LEGACY 0   // A/B: the round-3 branchy restatement (knn_tie_rows_wave_legacy)
 #endif
-#ifndef SWARM_DIAG_TIE_TWICE
-#define SWARM_DIAG_TIE_TWICE 0
+#ifndef SWARM_TIE_MEMO
+#define SWARM_TIE_MEMO 1   // acting waves keep each slot's last tie result keyed by its rank signature
 #endif
 #ifndef SWARM_DIAG_TIE_COUNT
 #define SWARM_DIAG_TIE_COUNT 0   // diagnostic builds: count tie-path entries (rows) and calls (waves)
@@ -191,17 +191,7 @@ __device__ inline int bit_sel_high(uint32_t m, int t) {
 __device__ unsigned long long g_swarm_tie_rows, g_swarm_tie_calls, g_swarm_knn_calls;
 __device__ unsigned int g_swarm_tie_env[4096];   // tie builds per acting wave (block * 4 + wave)
 #endif
-#ifndef SWARM_HEAP_NOINLINE
-#define SWARM_HEAP_NOINLINE 0   // A/B: the serial heap_select branch (depth limit) out of line
-#endif
-#ifndef SWARM_TIE_COLD
-#define SWARM_TIE_COLD 0        // A/B: the tie branch marked unlikely
-#endif
-#if SWARM_HEAP_NOINLINE
-static __device__ __attribute__((noinline)) void kv_heap_select_swap(KV* a, int first, int nth, int last) {
-#else
 static __device__ inline void kv_heap_select_swap(KV* a, int first, int nth, int last) {
-#endif
   kv_heap_select(a, first, nth + 1, last);
   kv_swap(a, first, nth);
 }
@@ -211,7 +201,7 @@ static __device__ inline void kv_heap_select_swap(KV* a, int first, int nth, int
 #define SWARM_TIE_INLINE inline
 #endif
 template <int NS, int GS>
-__device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
+__device__ SWARM_TIE_INLINE void knn_tie_rows_wave_legacy(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
                                                    const float* __restrict__ dn, KV* q) {
   constexpr int G = GS <= 8 ? 8 : 16;   // lanes per row
   constexpr int NG = 64 / G;
@@ -233,32 +223,6 @@ __device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsig
       if (depth == 0) { heap = true; break; }
       --depth;
       const int mid = first + (last - first) / 2;
-#if SWARM_TIE_FAST
-      // two lane hops per round: the four values the round reads (the one at `first` too) in one
-      // hop; the median-of-3 swap applied locally (v1 = the array after it, pv = its pivot); the
-      // partition's permutation composed with that swap and applied to the ORIGINAL row in one
-      // hop (v'' = v[swap(part(e))])
-      const float v0 = __shfl(v, gb + first), vx = __shfl(v, gb + first + 1), vy = __shfl(v, gb + mid),
-                  vz = __shfl(v, gb + last - 1);
-      int pick;   // kv_move_median_to_first(first, first + 1, mid, last - 1)
-      if (vx < vy) pick = (vy < vz) ? mid : ((vx < vz) ? last - 1 : first + 1);
-      else if (vx < vz) pick = first + 1;
-      else pick = (vy < vz) ? last - 1 : mid;
-      const float pv = pick == mid ? vy : (pick == first + 1 ? vx : vz);   // moved to `first`
-      const float v1 = e == first ? pv : (e == pick ? v0 : v);
-      const uint32_t lm = gballot(e > first && e < last && !(v1 < pv));
-      const uint32_t rm = gballot(e >= first && e < last && !(pv < v1));
-      const bool is_l = (lm >> e) & 1u, is_r = (rm >> e) & 1u;
-      const int tl = __popc(lm & ((1u << e) - 1u)) + 1;   // rank among the left stoppers
-      const int above = __popc(rm >> (e + 1));             // right stoppers after e
-      const int T = __popc(gballot(is_l && above >= tl));
-      int src = e;
-      if (is_l && tl <= T) src = bit_sel_high(rm, tl);
-      if (is_r && above + 1 <= T) src = bit_sel_low(lm, above + 1);
-      src = src == first ? pick : (src == pick ? first : src);
-      v = __shfl(v, gb + src);
-      id = __shfl(id, gb + src);
-#else
       const float vx = __shfl(v, gb + first + 1), vy = __shfl(v, gb + mid), vz = __shfl(v, gb + last - 1);
       int pick;   // kv_move_median_to_first(first, first + 1, mid, last - 1)
       if (vx < vy) pick = (vy < vz) ? mid : ((vx < vz) ? last - 1 : first + 1);
@@ -279,7 +243,6 @@ __device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsig
       if (is_r && above + 1 <= T) src = bit_sel_low(lm, above + 1);
       v = __shfl(v, gb + src);
       id = __shfl(id, gb + src);
-#endif
       int cut = __ffs(lm) - 1;
       if (T > 0) {
         cut = bit_sel_high(rm, T);
@@ -311,32 +274,161 @@ __device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsig
       id = __shfl(id, gb + src);
     }
     uint32_t mm = e < k ? (1u << id) : 0u;
-#if SWARM_TIE_FAST
-    // OR over the group's lanes by DPP inside the 16-lane row (no lane hop): quad xor 1, quad
-    // xor 2, half-row mirror (lanes i <-> 7 - i), and for 16-lane groups the row mirror
+#pragma unroll
+    for (int s = G / 2; s >= 1; s >>= 1) mm |= (uint32_t)__shfl_xor((int)mm, s);
+    if (e == 0) sm.knn[n] = mm;
+  }
+}
+
+
+// The boundary-tie rows, straight-line: the same restatement as knn_tie_rows_wave_legacy
+// (libstdc++ introselect on G lanes per row: median-of-3 swap, one-step unguarded partition,
+// rank-sort finish, serial heap_select at the depth limit) with every per-group decision a
+// select instead of a branch.  Rows whose count test fails in a formation that persists
+// (stacked agents keep a boundary tie every tick) run this every tick at one wave per SIMD,
+// where a wave issues one instruction per 4 cycles: its instruction count is the acting
+// launch's tail, hence the shape of a round:
+//  - one hop of four values (the one at `first` and the three median candidates); the median
+//    swap is applied locally (v1) and composed into the partition's gather;
+//  - the partition's swap pairs (L_t, R_t), t <= T, meet through LDS: each left stopper
+//    publishes its lane at slot rank - 1 of the group's L row, each right stopper at its rank
+//    of the R row, and a lane of a pair reads its partner's lane; the cut (L_1, or the smaller
+//    of R_T and L_(T+1)) is read from the same rows;
+//  - one hop of (value, id).
+// The rows' rounds run in lockstep; a group whose range is done keeps its lanes until the
+// wave's last group finishes.  The finish needs no data movement: the selected set is every id
+// left of `first` plus the range's elements whose stable rank (kv_insertion_sort's order) is
+// at most nth - first.  q: the wave's KV scratch, reused as the L / R rows (2 G ints per group).
+template <int NS, int GS>
+__device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
+                                                   const float* __restrict__ dn, KV* q) {
+  constexpr int G = GS <= 8 ? 8 : 16;   // lanes per row
+  constexpr int NG = 64 / G;
+  static_assert(NG * 2 * G <= 2 * NS * GS, "L / R rows fit the KV scratch");
+  const int g = lane / G, e = lane % G, gb = lane - e;
+  const int gb4 = gb << 2;
+  int* const lr = reinterpret_cast<int*>(q) + g * 2 * G;   // [0, G): L_t's lane at t - 1; [G, 2G): R_t's
+  auto gballot = [&](bool x) -> uint32_t {
+    return (uint32_t)((__builtin_amdgcn_ballot_w64(x) >> gb) & ((1ull << G) - 1ull));
+  };
+  auto any = [](bool x) -> bool { return __builtin_amdgcn_ballot_w64(x) != 0ull; };
+  // lane `from` of the group (ds_bpermute takes the lane modulo 64: out-of-range indices of
+  // finished groups read some lane and are discarded)
+  auto hop = [&](float x, int from) -> float {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute((from << 2) + gb4, __float_as_int(x)));
+  };
+  auto hopi = [&](int x, int from) -> int { return __builtin_amdgcn_ds_bpermute((from << 2) + gb4, x); };
+  const int nth = k - 1;
+  const int depth0 = 2 * floor_log2(N);
+  const uint32_t below = (1u << e) - 1u;
+  while (tb) {   // wave-uniform: up to NG tie rows per pass, group g takes the g-th remaining row
+    int bit = -1;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int b = tb ? __ffsll((long long)tb) - 1 : -1;
+      bit = i == g ? b : bit;
+      tb &= tb - 1ull;
+    }
+    const bool row = bit >= 0;
+    const int n = row ? bit / lpn : 0;
+    float v = (row && e < N) ? dn[n * GS + e] : 0.0f;
+    int id = e;
+    int first = 0, last = N, depth = depth0;
+    bool heap = false;
+    while (true) {   // wave-uniform trip count: the longest row's rounds
+      const bool open = row && !heap && last - first > 3;
+      heap = heap || (open && depth == 0);
+      const bool live = open && depth > 0;
+      if (!any(live)) break;
+      const int mid = first + (last - first) / 2;
+      const float v0 = hop(v, first), vx = hop(v, first + 1), vy = hop(v, mid), vz = hop(v, last - 1);
+      // kv_move_median_to_first(first, first + 1, mid, last - 1), as masks (no short circuits:
+      // the compiler keeps selects where nested conditionals become branches)
+      const bool xy = vx < vy, yz = vy < vz, xz = vx < vz;
+      const bool py = (xy && yz) || (!xy && !xz && !yz);
+      const bool pz = (xy && !yz && xz) || (!xy && !xz && yz);
+      const int pick = py ? mid : (pz ? last - 1 : first + 1);
+      const float pv = py ? vy : (pz ? vz : vx);   // the pivot, now at `first`
+      const float v1 = e == first ? pv : (e == pick ? v0 : v);
+      const bool in = live && e >= first && e < last;
+      const bool is_l = in && e != first && !(v1 < pv);   // left stopper (scan from first + 1)
+      const bool is_r = in && !(pv < v1);                 // right stopper (scan down to the pivot)
+      const uint32_t lm = gballot(is_l), rm = gballot(is_r);
+      const int tl = __popc(lm & below) + 1;      // rank among the left stoppers, ascending
+      const int above = __popc(rm >> (e + 1));    // right stoppers after e
+      const int tr = above + 1;                   // a right stopper's rank, descending
+      wave_lds_sync();                            // the previous round's reads are done
+      if (is_l) lr[tl - 1] = e;
+      if (is_r) lr[G + tr - 1] = e;
+      const int T = __popc(gballot(is_l && above >= tl));   // pairs with L_t < R_t
+      wave_lds_sync();
+      const bool take_r = is_r && tr <= T, take_l = is_l && tl <= T;
+      const int partner = lr[take_r ? tr - 1 : G + tl - 1];   // R_t reads L_t, L_t reads R_t
+      const int cut_r = lr[G + max(T, 1) - 1], cut_l = lr[min(T, G - 1)];
+      int src = (take_r || take_l) ? partner : e;
+      src = src == first ? pick : (src == pick ? first : src);   // through the median swap
+      src = live ? src : e;
+      v = hop(v, src);
+      id = hopi(id, src);
+      const int cut = T > 0 ? (__popc(lm) > T ? min(cut_r, cut_l) : cut_r) : __ffs(lm) - 1;
+      first = (live && cut <= nth) ? cut : first;
+      last = (live && cut > nth) ? cut : last;
+      depth -= live ? 1 : 0;
+    }
+    bool sel = e < k;   // heap rows: heap_select + swap leaves the set in [0, k)
+    if (any(heap)) {   // depth limit: heap_select + swap, serially (kv_nth_element)
+      KV* a = q + n * GS;
+      wave_lds_sync();
+      if (heap && e < N) a[e] = KV{v, id};
+      wave_lds_sync();
+      if (heap && e == 0) kv_heap_select_swap(a, first, nth, last);
+      wave_lds_sync();
+      if (heap && e < N) { v = a[e].v; id = a[e].i; }
+    }
+    {   // kv_insertion_sort of [first, last) (<= 3 elements) is stable: the range's element of
+        // stable rank r lands at first + r, so it is selected iff r <= nth - first
+      const bool in = e >= first && e < last;
+      int rank = 0;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int pj = first + j;
+        const float vj = hop(v, pj);
+        rank += (pj < last && (vj < v || (vj == v && pj < e))) ? 1 : 0;
+      }
+      sel = heap ? sel : (e < first || (in && rank <= nth - first));
+    }
+    // OR of the group's selected ids by DPP inside the 16-lane row: quad xor 1, quad xor 2,
+    // half-row mirror (i <-> 7 - i), and for 16-lane groups the row mirror
+    uint32_t mm = sel ? (1u << id) : 0u;
     mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0xB1, 0xF, 0xF, false);
     mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0x4E, 0xF, 0xF, false);
     mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0x141, 0xF, 0xF, false);
     if (G == 16) mm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mm, 0x140, 0xF, 0xF, false);
-#else
-#pragma unroll
-    for (int s = G / 2; s >= 1; s >>= 1) mm |= (uint32_t)__shfl_xor((int)mm, s);
-#endif
-    if (e == 0) sm.knn[n] = mm;
+    if (row && e == 0) sm.knn[n] = mm;
+    wave_lds_sync();   // the next pass rewrites q
   }
 }
 
 // kNN rows of every slot of the wave at once (NS <= 16): lane l serves slot n = l / LPN and
 // the candidates j = l % LPN + LPN i of n's graph.  Each pair distance is computed once
 // (the same fp32 expression as knn_mask_node), the graph's distance rows meet in LDS
-// (dn), and the set {j : #{l : d_l < d_j} < k} is assembled from wave ballots.  A slot
-// whose count test fails (a boundary tie) runs the introselect emulation in lane r = 0
+// (dn), and the set {j : #{l : d_l < d_j} < k} is assembled from wave ballots.  Slots
+// whose count test fails (a boundary tie) run the introselect restatement knn_tie_rows_wave
 // with its work space in LDS (q).  Writes sm.knn[n].
+// memo (acting waves; nullptr elsewhere): the last tie row's result per slot, keyed by the
+// row's rank signature: 4 bits of lt_j = #{l : d_l < d_j} per candidate.  d_a < d_b exactly
+// when lt_a < lt_b, and d_a == d_b exactly when lt_a == lt_b, so the signature fixes every
+// comparison introselect makes, hence its permutation and the selected ids: a tie row whose
+// signature equals the slot's memo takes the memo's set without running the tie path.  Stacked
+// agents keep a boundary tie on every tick while their distance ORDER changes rarely, and such
+// a slot otherwise re-runs the tie path every tick (the acting launch's tail).
 template <int NS, int GS>
-__device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, float* __restrict__ dn, KV* q) {
+__device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, float* __restrict__ dn, KV* q,
+                                      TieMemo<NS>* memo = nullptr) {
   constexpr int LPN = 64 / NS;          // lanes per slot
   constexpr int CPL = GS / LPN;         // candidates per lane
   static_assert(CPL >= 1 && GS % LPN == 0, "knn_masks_wave geometry");
+  static_assert(GS <= 16, "4-bit ranks of at most 16 candidates in the 64-bit signature");
   const int n = lane / LPN, r = lane % LPN;
   const int base = (GS < NS) ? (n / GS) * GS : 0;
   const int jn = (GS < NS) ? n % GS : n;
@@ -353,6 +445,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
   float row[GS];
   lds_load<GS>(dn + n * GS, row);
   uint32_t mask = 0;
+  uint32_t sig_lo = 0, sig_hi = 0;   // this lane's candidates' 4-bit ranks
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int j = r + LPN * i;
@@ -361,10 +454,35 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
     for (int l = 0; l < GS; ++l) lt += (l < N && row[l] < dv[i]) ? 1 : 0;
     const uint64_t b = __ballot(nvalid && j < N && lt < k);
     mask |= (uint32_t)((b >> (n * LPN)) & ((1ull << LPN) - 1ull)) << (LPN * i);
+    const uint32_t nib = j < N ? (uint32_t)lt : 0u;
+    if (LPN * i < 8) sig_lo |= nib << (4 * j);   // all of this i's candidates are below 8
+    else sig_hi |= nib << (4 * (j - 8));
   }
   const bool tie = r == 0 && nvalid && __popc(mask) != k;
-  if (r == 0) sm.knn[n] = nvalid ? mask : 0u;
-  const unsigned long long tb = __ballot(tie);
+  bool hit = false;
+  uint32_t hit_mask = 0u;
+  if (SWARM_TIE_MEMO && memo) {
+    // OR the slot's LPN lanes (aligned groups inside a 16-lane row): quad xor 1, quad xor 2,
+    // and for 8-lane slots the half-row mirror
+    sig_lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_lo, 0xB1, 0xF, 0xF, false);
+    sig_hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_hi, 0xB1, 0xF, 0xF, false);
+    if (LPN >= 4) {
+      sig_lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_lo, 0x4E, 0xF, 0xF, false);
+      sig_hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_hi, 0x4E, 0xF, 0xF, false);
+    }
+    if (LPN >= 8) {
+      sig_lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_lo, 0x141, 0xF, 0xF, false);
+      sig_hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_hi, 0x141, 0xF, 0xF, false);
+    }
+    static_assert(LPN == 4 || LPN == 8, "memo signature reduction covers 4- and 8-lane slots");
+    if (tie) {
+      hit = memo->sig_lo[n] == sig_lo && memo->sig_hi[n] == sig_hi;
+      hit_mask = memo->mask[n];
+    }
+  }
+  if (r == 0) sm.knn[n] = nvalid ? (hit ? hit_mask : mask) : 0u;
+  const bool run = tie && !hit;
+  const unsigned long long tb = __ballot(run);
 #if SWARM_DIAG_TIE_COUNT
   if (lane == 0) {
     atomicAdd(&g_swarm_knn_calls, 1ull);
@@ -375,15 +493,35 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
     }
   }
 #endif
-  if (!SWARM_DIAG_NO_TIE && (SWARM_TIE_COLD ? __builtin_expect(tb != 0ull, 0) : tb != 0ull)) {
+  if (!SWARM_DIAG_NO_TIE && tb != 0ull) {
     // boundary ties: the introselect restatement, G lanes per row
+#if SWARM_STAMPS   // stamps build: per-wave tie-path entries (slot 27) and s_memtime cycles in it (slot 28)
+    const long long s0 = clock64();
+#endif
     wave_lds_sync();
-    knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
-#if SWARM_DIAG_TIE_TWICE   // timing diagnostic: the same (idempotent) tie path a second time
+    if (SWARM_TIE_LEGACY) knn_tie_rows_wave_legacy<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
+    else knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
     wave_lds_sync();
-    knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
+    if (SWARM_TIE_MEMO && memo && run) {
+      memo->sig_lo[n] = sig_lo;
+      memo->sig_hi[n] = sig_hi;
+      memo->mask[n] = sm.knn[n];
+    }
+#if SWARM_STAMPS
+    wave_lds_sync();
+    const long long s1 = clock64();
+    if (g_swarm_stamps && lane == 0) {
+      unsigned long long* ws = g_swarm_stamps + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32;
+      ws[27] += 1ull;
+      ws[28] += (unsigned long long)(s1 - s0);
+      if ((unsigned long long)(s1 - s0) > ws[26]) ws[26] = (unsigned long long)(s1 - s0);
+    }
 #endif
   }
+#if SWARM_STAMPS
+  if (SWARM_TIE_MEMO && memo && g_swarm_stamps && lane == 0 && __ballot(hit) != 0ull)   // slot 18: memo hits
+    g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + 18] += 1ull;
+#endif
 }
 
 // Full GCN.forward.  F.x must hold the lane's features (zero for nodes >= N).  P is the
@@ -451,7 +589,7 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
   if (graph == SWARM_GRAPH_KNN) {
     // work space in the wave's T / R rows (free until the aggregation writes T)
     if constexpr (NS <= 16) {
-      knn_masks_wave<NS, GS>(d.lane, N, k, sm, &V.T[0][0], reinterpret_cast<KV*>(&V.R[0][0]));
+      knn_masks_wave<NS, GS>(d.lane, N, k, sm, &V.T[0][0], reinterpret_cast<KV*>(&V.R[0][0]), V.memo);
     } else {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {

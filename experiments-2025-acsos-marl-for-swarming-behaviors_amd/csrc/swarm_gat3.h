@@ -56,7 +56,7 @@ __device__ inline void gat3_forward(const float* __restrict__ P, const DGeom<NS>
   // neighbour masks (dl_forward's graph phase; T / R rows are free scratch until layer 1)
   if (graph == SWARM_GRAPH_KNN) {
     if constexpr (NS <= 16) {
-      knn_masks_wave<NS, NS>(d.lane, N, k, sm, &V.T[0][0], reinterpret_cast<KV*>(&V.R[0][0]));
+      knn_masks_wave<NS, NS>(d.lane, N, k, sm, &V.T[0][0], reinterpret_cast<KV*>(&V.R[0][0]), V.memo);
     } else {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {

@@ -114,6 +114,17 @@ struct WSmall {
   uint32_t knn[NS];
 };
 
+// an acting wave's kNN tie memo (knn_masks_wave): per slot, the rank signature of the last
+// tie row it resolved and that row's neighbour set; sig_lo = ~0 marks an empty entry (no row
+// has every rank 15)
+template <int NS>
+struct TieMemo {
+  uint32_t sig_lo[NS], sig_hi[NS], mask[NS];
+  __device__ void clear(int lane) {
+    for (int n = lane; n < NS; n += 64) sig_lo[n] = ~0u;
+  }
+};
+
 // what one wave's forward reads and writes in LDS: NS rows of H, T (tanh out) and
 // R (relu out) — private scratch when acting, rows of the TD block's images in TD
 template <int NS>
@@ -122,13 +133,15 @@ struct WView {
   float (*T)[kRow];
   float (*R)[kRow];
   WSmall<NS>* sm;
+  TieMemo<NS>* memo = nullptr;   // acting waves only
 };
 
 template <int NS>
 struct WScratch {
   float H[NS][kRow], T[NS][kRow], R[NS][kRow];
   WSmall<NS> sm;
-  __device__ WView<NS> view() { return WView<NS>{H, T, R, &sm}; }
+  TieMemo<NS> memo;
+  __device__ WView<NS> view() { return WView<NS>{H, T, R, &sm, &memo}; }
 };
 
 template <int K>

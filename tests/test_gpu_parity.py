@@ -172,13 +172,22 @@ def test_knn_graph_bit_exact(sw, N, k):
 def test_acting_knn_ties_match_torch_topk(sw, golden_weights, N, k):
     """The acting path's kNN build (knn_masks_wave, boundary ties through the G-lane
     introselect restatement knn_tie_rows_wave) on tie-heavy formations: lattice positions in
-    multiples of 1/8 (exact, mostly equal distances; duplicated agents) give edge multiplicities
+    multiples of 1/8 (exact, mostly equal distances; duplicated agents) and random positions with
+    stacked agents give edge multiplicities
     equal to torch.topk's sets (oracle knn_sets) bit for bit.  N = 15, k = 9 carries
     knn_select.HEAP_PATH_ROW in env 0 (the depth-limit heap_select branch)."""
     from oracle import knn_select
-    B = 256
+    B = 1024
     g = torch.Generator().manual_seed(N * 100 + k)
     pos = torch.randint(-3, 4, (B, N, 2), generator=g).float() * 0.125
+    # the other half: random positions with stacked agents (an agent copied onto another one,
+    # the formation that keeps a boundary tie on every tick of a rollout)
+    h = B // 2
+    pos[h:] = torch.rand(B - h, N, 2, generator=g) * 2.0 - 1.0
+    for _ in range(max(1, N // 3)):
+        src = torch.randint(0, N, (B - h,), generator=g)
+        dst = torch.randint(0, N, (B - h,), generator=g)
+        pos[torch.arange(h, B), dst] = pos[torch.arange(h, B), src]
     if (N, k) == (15, 9):
         vals, _ = knn_select.HEAP_PATH_ROW
         pos[0, :, 0] = torch.tensor(vals, dtype=torch.float32) * 0.125
@@ -194,7 +203,8 @@ def test_acting_knn_ties_match_torch_topk(sw, golden_weights, N, k):
     assert torch.equal(mult.view(B, N, N).cpu().float(), O.multiplicity_knn(O.knn_sets(pos, k)))
     if k < N and N >= 5:   # the tie path really ran: rows whose k-th and (k+1)-th distances are equal
         d = torch.linalg.norm(pos[:, None, :, :] - pos[:, :, None, :], dim=-1).sort(dim=-1).values
-        assert int((d[..., k - 1] == d[..., k]).sum()) > B // 8
+        assert int((d[:h, :, k - 1] == d[:h, :, k]).sum()) > h // 8
+        assert int((d[h:, :, k - 1] == d[h:, :, k]).sum()) > 0
 
 
 @pytest.mark.parametrize("N,radius", [(5, 0.15), (8, 0.15), (8, 0.3), (12, 0.2), (16, 0.25), (29, 0.2)])
@@ -377,6 +387,46 @@ def test_rollout_equals_single_ticks(sw, golden_weights, graph):
     assert torch.equal(a.state, b.state)
     assert torch.allclose(r["reward"], rew, rtol=1e-6, atol=1e-5)
     assert torch.equal(r["traj_pos"][-1], a.state[..., :2])
+
+
+@pytest.mark.parametrize("N,k", [(8, 5), (5, 3), (12, 5), (16, 7)])
+def test_rollout_knn_tie_memo_equals_single_ticks(sw, golden_weights, N, k):
+    """Stacked agents (zero pair force below kMinDist) keep boundary ties tick after tick.  The
+    rollout resolves a tie row whose rank signature repeats from its slot's memo
+    (knn_masks_wave); single act ticks run the tie path every time (no memo), and their tie rows
+    are pinned against torch.topk by test_acting_knn_ties_match_torch_topk.  Same trajectories,
+    bit for bit, over 30 ticks of lattice and stacked formations."""
+    B, T = 256, 30
+    g = torch.Generator().manual_seed(N * 7 + k)
+    pos = torch.rand(B, N, 2, generator=g) * 1.6 - 0.8
+    pos[: B // 2] = torch.randint(-3, 4, (B // 2, N, 2), generator=g).float() * 0.125
+    for _ in range(max(1, N // 3)):
+        src = torch.randint(0, N, (B,), generator=g)
+        dst = torch.randint(0, N, (B,), generator=g)
+        pos[torch.arange(B), dst] = pos[torch.arange(B), src]
+    vel = torch.zeros(B, N, 2)
+    p = _params(golden_weights, "go_to", 3)
+    kw = dict(seed=4, params=p, graph="knn", knn_k=k, learn=False, eps=0.0)
+    a = sw.SwarmEngine("GoTo", N, B, **kw)
+    b = sw.SwarmEngine("GoTo", N, B, **kw)
+    for e in (a, b):
+        e.reset(0)
+        e.set_state(pos, vel)
+    rew = torch.zeros(B, N, device="cuda")
+    for t in range(T):
+        b.ctrl[0] = t
+        b.act(push=False)
+        rew += b.reward
+    r = a.rollout(T, tick0=0, eps=0.0, traj=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.state, b.state)
+    assert torch.allclose(r["reward"], rew, rtol=1e-6, atol=1e-5)
+    # the formations tie at the k-th distance at the start, and some still do on the last tick
+    def ties(q):
+        d = torch.linalg.norm(q[:, None, :, :] - q[:, :, None, :], dim=-1).sort(dim=-1).values
+        return int((d[..., k - 1] == d[..., k]).sum())
+    assert ties(pos) > B // 8
+    assert ties(a.state[..., :2].cpu()) > 0
 
 
 # ------------------------------------------------------------------ learner
