@@ -225,6 +225,67 @@ def topk_smallest_set_lanes(values, k):
     return sorted(j for _, j in q[:k])
 
 
+def topk_smallest_set_slots(values, k):
+    """The round-3 device form (csrc/swarm_dl.h knn_tie_rows_wave): the same rounds as
+    nth_element_lanes, with the swap partners found through rank slots (each left stopper
+    publishes its index at its rank in an L row, each right stopper in an R row; a pair's
+    members read each other) and the cut read from those rows; the closing insertion sort is
+    replaced by its set: [0, first) plus the range elements of stable rank <= nth - first."""
+    n = len(values)
+    if k > n:
+        raise RuntimeError("selected index k out of range")
+    a = [(float(values[j]), j) for j in range(n)]
+    nth = k - 1
+    first, last = 0, n
+    depth = 2 * (n.bit_length() - 1)
+    heap = False
+    while last - first > 3:
+        if depth == 0:
+            heap = True
+            break
+        depth -= 1
+        mid = first + (last - first) // 2
+        x, y, z = first + 1, mid, last - 1
+        vx, vy, vz = a[x][0], a[y][0], a[z][0]
+        xy, yz, xz = vx < vy, vy < vz, vx < vz
+        py = (xy and yz) or (not xy and not xz and not yz)
+        pz = (xy and not yz and xz) or (not xy and not xz and yz)
+        pick = y if py else (z if pz else x)
+        a[first], a[pick] = a[pick], a[first]
+        pv = a[first][0]
+        L = [e for e in range(first + 1, last) if not a[e][0] < pv]            # ascending
+        R = [e for e in reversed(range(first, last)) if not pv < a[e][0]]      # descending
+        T = sum(1 for t in range(min(len(L), len(R))) if L[t] < R[t])
+        src = list(range(n))
+        for t in range(T):                 # a lane that is R_t wins over being L_t', as on the device
+            src[L[t]] = R[t]
+        for t in range(T):
+            src[R[t]] = L[t]
+        a = [a[s] for s in src]
+        cut = L[0] if T == 0 else (min(R[T - 1], L[T]) if len(L) > T else R[T - 1])
+        if cut <= nth:
+            first = cut
+        else:
+            last = cut
+    if heap:
+        _heap_select(a, first, nth + 1, last)
+        a[first], a[nth] = a[nth], a[first]
+        return sorted(j for _, j in a[:k])
+    sel = list(range(first))
+    for e in range(first, last):
+        rank = sum(1 for j in range(first, last) if a[j][0] < a[e][0] or (a[j][0] == a[e][0] and j < e))
+        if rank <= nth - first:
+            sel.append(e)
+    return sorted(a[e][1] for e in sel)
+
+
+def rank_signature(values):
+    """The tie memo's key (csrc/swarm_dl.h knn_masks_wave): lt_j = #{l : d_l < d_j} per
+    element.  d_a < d_b iff lt_a < lt_b and d_a == d_b iff lt_a == lt_b, so the signature fixes
+    every comparison introselect makes and with it the selected set."""
+    return tuple(sum(1 for w in values if w < v) for v in values)
+
+
 # A boundary-tie row (n = 15, k = 9: two 9s straddle the k-th place) whose introselect runs out
 # of depth and ends in heap_select (found by search; exercised on the GPU by
 # tests/test_gpu_parity.py test_acting_knn_ties_match_torch_topk)

@@ -68,6 +68,57 @@ def test_lane_parallel_topk_restatement_matches_torch():
     assert knn_select.topk_smallest_set_lanes(vals, k) == knn_select.topk_smallest_set(vals, k) == want
 
 
+def test_slot_exchange_topk_restatement_matches_torch():
+    """Round 3's straight-line tie path (partners through rank slots, the finish as a stable-rank
+    set; knn_select.topk_smallest_set_slots) selects torch.topk's set on the committed fixture,
+    3,000 fresh tie-heavy rows and the heap_select row."""
+    import random
+    z = np.load(os.path.join(ROOT, "tests", "golden", "topk_ties.npz"))
+    for row, (n, k), s in zip(z["dist"], z["nk"], z["sets"]):
+        assert knn_select.topk_smallest_set_slots(row[:n], int(k)) == sorted(np.where(s)[0].tolist())
+    rng = random.Random(13)
+    for trial in range(3000):
+        n = rng.randint(4, 16)
+        k = rng.randint(1, n)
+        vals = ([float(rng.randint(0, 3)) for _ in range(n)] if trial % 2 else
+                [rng.choice([0.15, 0.3, 0.2121, 0.3354]) for _ in range(n)])
+        d = torch.tensor(vals, dtype=torch.float32)
+        want = sorted(torch.topk(d, k, largest=False).indices.tolist())
+        assert knn_select.topk_smallest_set_slots(d.tolist(), k) == want, (vals, k)
+    vals, k = knn_select.HEAP_PATH_ROW
+    assert knn_select.topk_smallest_set_slots(vals, k) == knn_select.topk_smallest_set(vals, k)
+
+
+def test_rank_signature_fixes_the_topk_set():
+    """The acting rollout's tie memo (csrc/swarm_dl.h knn_masks_wave) reuses a slot's last tie
+    result when the row's rank signature lt_j = #{l : d_l < d_j} repeats.  Pinned against the
+    reference's own call, torch.topk: rows mapped through random strictly increasing value maps
+    keep their signature and their set, and across 20,000 random tie-heavy rows every signature
+    has one set."""
+    import random
+    rng = random.Random(17)
+    seen = {}
+    for trial in range(20000):
+        n = rng.randint(4, 10)
+        k = rng.randint(1, n - 1)
+        vals = [float(rng.randint(0, 4)) for _ in range(n)]
+        d = torch.tensor(vals, dtype=torch.float32)
+        want = sorted(torch.topk(d, k, largest=False).indices.tolist())
+        sig = knn_select.rank_signature(vals)
+        key = (n, k, sig)
+        assert seen.setdefault(key, want) == want, (vals, k)
+        if trial % 10 == 0:   # a strictly increasing map of the distinct values
+            levels = sorted(set(vals))
+            new = sorted(rng.uniform(0.0, 2.0) for _ in levels)
+            if len(set(new)) == len(new):
+                f = dict(zip(levels, new))
+                mapped = [f[v] for v in vals]
+                assert knn_select.rank_signature(mapped) == sig
+                dm = torch.tensor(mapped, dtype=torch.float32)
+                assert sorted(torch.topk(dm, k, largest=False).indices.tolist()) == want, (vals, mapped, k)
+    assert len(seen) > 1000
+
+
 def test_host_topk_matches_torch_fixture():
     """The C++ selection the kernels run (swarm_knn.h), compiled for the host."""
     L, lib = _host_lib()
