@@ -331,7 +331,15 @@ def main():
                 per.append(e0.elapsed_time(e1) * 1e3 / kchain)
             return float(np.median(per))   # microseconds per launch
 
-        if fused:
+        if fused and eng.tick_reduce:
+            # one launch per tick: the slab reduce and the ctrl advance run inside the tick kernel
+            eng.reset()
+            kt["tick_kernel"] = chain_us(eng.launch_tick, 40)
+            kt["ctrl_advance_kernel (an empty launch's period, for scale)"] = chain_us(eng.advance, 40)
+            eng.flush()
+            eng.reset()
+            assert eng.handoff_errors() == 0, "fused tick: a hand-off or reduce wait hit its bound"
+        elif fused:
             eng.reset()
             t_pair = chain_us(lambda: (eng.launch_tick(), eng.advance()), 40)
             t_adv = chain_us(eng.advance, 40)
@@ -425,7 +433,8 @@ def main():
                            "parallelism": f"env-sharded dp{world}" + ("" if not distributed else
                                           " + xGMI peer grad all-reduce" if peer is not None else
                                           f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce"),
-                           "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
+                           "hipgraph": graph is not None, "tick": ("1 launch (slab reduce + ctrl advance in-kernel)" if fused and eng.tick_reduce else
+                                    "1 launch + reduce" if fused else "3 launches"),
                            "allreduce": allreduce, "allreduce_paths": both, "rank_errors": rank_errors,
                            "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu, "acting_only": acting,

@@ -38,6 +38,7 @@ struct ActArgs {
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
   int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
   unsigned long long* ho_rec;   // fused tick: [B][ho_stride_granules(N)] hand-off records (swarm_common.h)
+  unsigned long long* red_ws;   // one-launch tick (swarm_red.h): the workspace's counter words
 };
 
 constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
@@ -63,7 +64,8 @@ struct ActSmem {
 // training-tick kernel runs acting blocks beside TD blocks).
 // HO: fused-tick hand-off publishing (swarm_tick.hip only).  NET: SWARM_NET_GCN (the D-layout
 // MFMA forward) or SWARM_NET_GAT3 (swarm_gat3.h; acting only, no learner prologue)
-template <int NS, int MODE, int SCEN, int SPEC, bool HO = false, int NET = SWARM_NET_GCN>
+// RED: one-launch tick (swarm_red.h): the block counts itself past its prologue
+template <int NS, int MODE, int SCEN, int SPEC, bool HO = false, int NET = SWARM_NET_GCN, bool RED = false>
 __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int nvb,
                                          const swarm_ctrl* __restrict__ ctrl, float* state, const float* grad,
                                          const float* w_cur, const float* m_cur, const float* v_cur, int B, int N,
@@ -74,8 +76,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   float* red = S.red;
   SWARM_RTSTAMP(30);
   SWARM_STAMP(0);
-#if SWARM_STAMPS   // slot 29: where the wave runs (HW_ID in the low word, XCC_ID in the high word)
-  if (g_swarm_stamps && (threadIdx.x & 63) == 0)
+#if SWARM_STAMPS   // rollouts, slot 29: where the wave runs (HW_ID in the low word, XCC_ID in the high word)
+  if (MODE == MODE_ROLLOUT && g_swarm_stamps && (threadIdx.x & 63) == 0)
     g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + 29] =
         (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
         ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
@@ -130,6 +132,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // flight together instead of dependent loads behind branches)
   swarm_ctrl cc = {};
   if (MODE == MODE_TICK) cc = *ctrl;
+  unsigned long long red_epoch = 0ull;   // RED: this launch's epoch, with ctrl's round trip
+  if constexpr (RED) red_epoch = red_epoch_load(A.red_ws);
   uint32_t tick = A.tick0;
   float eps = A.eps;
   uint32_t slot = 0;
@@ -195,6 +199,9 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     ps.store(Pw, threadIdx.x);
   }
   __syncthreads();   // weight image complete
+  if constexpr (RED) {   // ctrl, grad and _cur are read (block 0's _nxt stores are its own, swarm_red.h)
+    if (threadIdx.x == 0) red_count(A.red_ws + kWsActPro, red_epoch);
+  }
   const float* P = Pw;
   SWARM_STAMP(1);
 #if SWARM_DIAG_ACT   // diagnostic A/B builds only: acting waves stop after the optimizer step

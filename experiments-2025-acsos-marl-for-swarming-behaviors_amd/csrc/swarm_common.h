@@ -208,6 +208,18 @@ __device__ inline unsigned long long ld_granule(const unsigned long long* g) {
   return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// one-launch tick (swarm_red.h): counters in the tick workspace, 64-bit words
+// {epoch << 16 | count}.  The epoch advances once per one-launch tick (its control role), so a
+// count never carries over from an earlier launch whatever happens to ctrl in between: an
+// incrementer raises the word to its epoch's base (atomicMax) before adding one.
+constexpr int kWsEpoch = 16, kWsActPro = 32, kWsTdDone = 48;   // u64 word indices, one 128-B line each
+__device__ inline unsigned long long red_epoch_load(const unsigned long long* ws) {
+  return __hip_atomic_load(ws + kWsEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void red_count(unsigned long long* w, unsigned long long epoch) {
+  __hip_atomic_fetch_max(w, epoch << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // ---------------------------------------------------------------- small math
 __host__ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * kLeakySlope; }
 

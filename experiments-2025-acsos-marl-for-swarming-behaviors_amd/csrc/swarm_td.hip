@@ -8,6 +8,7 @@
 
 #include "swarm_tdk.h"
 #include "swarm_peer.h"
+#include "swarm_red.h"
 
 namespace swarm {
 
@@ -46,16 +47,8 @@ struct ReduceArgs {
 // reproducible run to run.  Advance mode adds one control block (the last): it prepares
 // and stores the whole ctrl update (Adam scalars of the next step in double, the next
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
-#ifndef SWARM_RED_COLS
-#define SWARM_RED_COLS 16
-#endif
-#ifndef SWARM_RED_GROUPS
-#define SWARM_RED_GROUPS 64
-#endif
-// The ping-pong copy-back (w / m / v _nxt -> _cur) runs in three extra blocks of its own (one
-// array each, a float4 per thread) beside the column blocks (1); 0 = in waves 0-2 of every column
-// block after its slab loads (round 2).  14.24 -> 14.09 us per tick, three interleaved pairs
-// (profiles/r03_ab_reduce.jsonl)
+// kRedCols = 16 columns x kRedGroups = 64 slab groups per block (swarm_red.h, shared with the
+// one-launch tick's column roles, which must sum in this exact order)
 #ifndef SWARM_RED_COPY_BLOCKS
 #define SWARM_RED_COPY_BLOCKS 1
 #endif
@@ -65,11 +58,7 @@ constexpr int kRedCopyBlocks = SWARM_RED_COPY_BLOCKS ? 3 : 0;
 #ifndef SWARM_RED_DPP
 #define SWARM_RED_DPP 0
 #endif
-constexpr int kRedCols = SWARM_RED_COLS;
-constexpr int kRedGroups = SWARM_RED_GROUPS;
-constexpr int kRedRuns = kRedGroups / 8;   // first combine level: runs of 8 group sums
 static_assert(kRedGroups % 8 == 0 && kRedCols * kRedGroups <= 1024, "reduce geometry");
-constexpr int kRedColBlocks = (N_PARAMS + 1 + kRedCols - 1) / kRedCols;
 static_assert(kRedColBlocks <= kPeerSeqRegion, "peer seq region");
 // slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start.
 // PEER = 1 (swarm_reduce_advance_peer): each column block then exchanges its 16 column sums with
@@ -91,55 +80,10 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     if ((int)threadIdx.x < N_PARAMS_PAD / 4) dst[threadIdx.x] = src[threadIdx.x];
     return;
   }
-  if ((int)blockIdx.x == kRedColBlocks) {   // advance mode: the control block
-    // thread 0 advances the counters and the Adam scalars; thread 64 (another wave) derives
-    // the next tick's sampling key; both read ctrl before the barrier, write after it
-    const int t = threadIdx.x;
-    uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
-    double b1p = 1.0, b2p = 1.0;
-    float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
-    SampleKey nk = {};
-    uint32_t nk_n = 0, nk_tick = 0;
-    const uint32_t cap = (uint32_t)A.capacity;
-    if (t == 0) {
-      // a held rank (peer_hold: an expired exchange wait) applied no step this tick
-      c_trained = C->peer_hold ? 0u : C->trained;
-      c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
-      b1p = ctrl_get_double(C, CTRL_B1POW);
-      b2p = ctrl_get_double(C, CTRL_B2POW);
-      if (c_trained) {   // the step this tick's act kernel applied
-        b1p = b1p * (double)A.hp.beta1;
-        b2p = b2p * (double)A.hp.beta2;
-        adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
-      }
-    } else if (t == 64) {
-      const uint32_t filled = C->filled_slots;
-      const uint32_t f1 = filled + 1 < cap ? filled + 1 : cap;   // filled after this tick
-      nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;       // graphs the next tick samples from
-      nk_tick = C->tick + 1;
-      nk = sample_key(nk_n, A.k0, A.k1, nk_tick);
-    }
-    __syncthreads();
-    if (t == 0) {   // record the pending update, advance the tick
-      const uint32_t valid_slots = c_filled + 1 < cap ? c_filled + 1 : cap;
-      const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
-      if (c_trained) {
-        C->adam_step = c_step + 1;
-        ctrl_set_double(C, CTRL_B1POW, b1p);
-        ctrl_set_double(C, CTRL_B2POW, b2p);
-        C->adam_step_size = next_step_size;
-        C->adam_inv_bc2 = next_inv_bc2;
-      }
-      C->trained = trained;
-      C->tick = c_tick + 1;
-      C->write_slot = (c_slot + 1) % cap;
-      C->filled_slots = valid_slots;
-    } else if (t == 64) {
-      C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
-      C->sample_bits = (uint32_t)nk.bits;
-      C->sample_n = nk_n;
-      C->sample_tick = nk_tick;
-    }
+  if ((int)blockIdx.x == kRedColBlocks) {   // advance mode: the control block (swarm_red.h)
+    RedCtrl rc;
+    rc.capacity = A.capacity; rc.B = A.B; rc.batch = A.batch; rc.hp = A.hp; rc.k0 = A.k0; rc.k1 = A.k1;
+    red_control(C, rc);
     return;
   }
   const int c = threadIdx.x % kRedCols;
@@ -148,7 +92,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   const int per = (n_slabs + kRedGroups - 1) / kRedGroups;
   const int b0 = q * per, b1 = min(n_slabs, b0 + per);
   // first chunk of this thread's slab column in flight before anything else
-  constexpr int kChunk = 8;
+  constexpr int kChunk = kRedChunk;
   float v0[kChunk];
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)

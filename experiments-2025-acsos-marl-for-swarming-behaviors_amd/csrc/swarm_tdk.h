@@ -113,6 +113,7 @@ struct TdFused {
   swarm_adam_cfg hp;
   const unsigned long long* ho_rec;   // [B][ho_stride_granules(N)] tagged hand-off records
   uint32_t* ho_err;                   // bounded-wait overruns (0 in a correct run)
+  unsigned long long* red_ws;         // one-launch tick (swarm_red.h): the workspace's counter words
 };
 #ifndef SWARM_HO_SPIN_LIMIT
 #define SWARM_HO_SPIN_LIMIT (1 << 18)
@@ -166,7 +167,15 @@ __device__ inline void drop_overrun(const bool (&okc)[DGeom<NS>::CT], bool (&dro
     if (bad[ct]) { drop[ct] = true; nv[ct] = false; }
 }
 
-template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
+// a TD block's slab granules are issued -> count it (no drain: the granules carry their own tags)
+__device__ inline void red_td_done_cnt(unsigned long long* ws, unsigned long long epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) red_count(ws + kWsTdDone, epoch);
+}
+
+// RED (fused only): the one-launch tick (swarm_red.h): the slab goes out as tagged granules and
+// the block counts itself done, for the acting blocks' reduce roles
+template <int NS, int GS, int SPEC, bool FUSED = false, bool RED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
                                         const float* rs_next, const float* rr, const uint8_t* ra, int S, int B,
                                         int N, int capacity, const TdArgs& A, const TdFused& X,
@@ -189,8 +198,16 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.target_view(wi);
   const int lane = d.lane, c = d.c, p = d.p;
-  // this block's slab column q (swarm_common.h slab_index: column-block major)
-  auto gslab = [&](int q) { return A.slabs + slab_index(q, vb, A.n_slabs); };
+  // this block's slab column q (swarm_common.h slab_index: column-block major); RED: granules
+  static_assert(!RED || FUSED, "the one-launch tick is a fused tick");
+  uint32_t red_tag = 0u;   // RED: this tick's tag (tick + 1), set once ctrl is read
+  auto sst = [&](int q, float v) {
+    if constexpr (RED) {
+      st_granule(reinterpret_cast<unsigned long long*>(A.slabs) + slab_index(q, vb, A.n_slabs), red_tag, __float_as_uint(v));
+    } else {
+      slab_st(A.slabs + slab_index(q, vb, A.n_slabs), v);
+    }
+  };
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
@@ -210,6 +227,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // write_slot, the batch size S, the Adam hyper-parameters) made opaque here, so they are
   // loaded with the first scalar wait instead of being re-fetched at a later first use behind a
   // second one (a kernarg / ctrl round trip on the TD chain)
+  unsigned long long red_epoch = 0ull;
+  if constexpr (RED) {
+    red_tag = cc.tick + 1u;
+    red_epoch = red_epoch_load(X.red_ws);
+  }
   swarm_adam_cfg hp = X.hp;
   int32_t* sample_out = A.sample_out;
   const unsigned long long* ho_rec = X.ho_rec;
@@ -275,7 +297,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
   if (n_graphs < (uint32_t)S) {
-    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) slab_st(gslab(q), 0.0f);
+    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) sst(q, 0.0f);
+    if constexpr (RED) red_td_done_cnt(X.red_ws, red_epoch);
     return;
   }
   if (sample_out && online && p == 0) {
@@ -632,7 +655,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       if (job == 0) {
         const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) slab_st(gslab(OFF_W1 + acc_row(r, h) * kHidden + col), dW1[r]);
+        for (int r = 0; r < 16; ++r) sst(OFF_W1 + acc_row(r, h) * kHidden + col, dW1[r]);
       } else if (job == 1) {
         f32x16 dW2 = {};
 #pragma unroll
@@ -644,7 +667,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int a = acc_row(r, h);
-          if (a < kActions) slab_st(gslab(OFF_W2 + a * kHidden + col), dW2[r]);
+          if (a < kActions) sst(OFF_W2 + a * kHidden + col, dW2[r]);
         }
         if (lane < kActions || lane == 63) {   // every read issued before the ordered sum
           float v[kTdRows];
@@ -653,7 +676,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
           float acc = v[0];
 #pragma unroll
           for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-          slab_st(gslab(lane == 63 ? N_PARAMS : OFF_B2 + lane), acc);
+          sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
         }
       } else {
         if (lane < kHidden) {
@@ -663,7 +686,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
           float acc = v[0];
 #pragma unroll
           for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-          slab_st(gslab(OFF_B1 + lane), acc);
+          sst(OFF_B1 + lane, acc);
         }
       }
     }
@@ -686,7 +709,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         }
         if (c < kFeat) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) slab_st(gslab(OFF_W + (16 * t + 4 * p + r) * kFeat + c), acc[r]);
+          for (int r = 0; r < 4; ++r) sst(OFF_W + (16 * t + 4 * p + r) * kFeat + c, acc[r]);
         }
       } else if (job == 2) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
         const float* da = h == 0 ? TB.das : TB.dad;
@@ -696,7 +719,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        slab_st(gslab((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col), acc);
+        sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, acc);
       } else if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
@@ -704,12 +727,13 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        slab_st(gslab(OFF_BIAS + lane), acc);
+        sst(OFF_BIAS + lane, acc);
       }
     }
   }
   SWARM_STAMP(7);
   SWARM_RTSTAMP(9);
+  if constexpr (RED) red_td_done_cnt(X.red_ws, red_epoch);
 }
 
 }  // namespace swarm
