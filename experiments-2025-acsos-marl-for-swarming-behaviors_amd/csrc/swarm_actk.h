@@ -171,6 +171,19 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 #if SWARM_PIN
   asm volatile("" : "+s"(rp_s), "+s"(rp_sn), "+s"(rp_r), "+s"(rp_a), "+s"(o_rew), "+s"(o_avg), "+s"(o_hits), "+s"(smp));
 #endif
+  // fused tick: s of a sampled transition is the state loaded above, so it is published now, a
+  // whole optimizer step and forward ahead of a: the waiting online TD wave runs its forward on
+  // s (and its gq-free backward once a lands) while this wave computes (swarm_tdk.h, pre path)
+  unsigned long long* ho_r = nullptr;
+  const uint32_t ho_tag = cc.tick + 1u;
+  if (MODE == MODE_TICK && HO && ho_pub) {
+    ho_r = A.ho_rec + (size_t)d.gid * ho_stride_granules(N);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      if (valid[ct])
+        st_granule(ho_r + 4 * (16 * ct + c) + p, ho_tag,
+                   __float_as_uint(p == 0 ? px[ct] : (p == 1 ? py[ct] : (p == 2 ? vx[ct] : vy[ct]))));
+  }
   if (MODE == MODE_TICK && NET == SWARM_NET_GCN && (kLearnCT || A.learn)) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
@@ -265,25 +278,12 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 
     // fused tick: this env's transition is in the tick's TD batch -> publish it as tagged
     // write-through granules as soon as each part exists (swarm_common.h hand-off record):
-    // s and a now (the online TD wave starts its forward), s' after the integrator (the
-    // target TD wave's forward input), r after the reward (needed only for y)
-    unsigned long long* ho_r = nullptr;
-    const uint32_t ho_tag = cc.tick + 1u;
-    if (MODE == MODE_TICK && HO && ho_pub) {
-      ho_r = A.ho_rec + (size_t)d.gid * ho_stride_granules(N);
+    // s at the prologue (above), a now (the online TD wave's gq-free backward), s' after the
+    // integrator (the target TD wave's forward input), r after the reward (needed only for y)
+    if (MODE == MODE_TICK && HO && ho_r) {
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int n = 16 * ct + c;
-        if (valid[ct]) {
-          if (p == 0) st_granule(ho_r + 4 * n, ho_tag, __float_as_uint(px[ct]));
-          else if (p == 1) st_granule(ho_r + 4 * n + 1, ho_tag, __float_as_uint(py[ct]));
-          else if (p == 2) st_granule(ho_r + 4 * n + 2, ho_tag, __float_as_uint(vx[ct]));
-          else {
-            st_granule(ho_r + 4 * n + 3, ho_tag, __float_as_uint(vy[ct]));
-            st_granule(ho_r + 9 * N + n, ho_tag, (uint32_t)action[ct]);
-          }
-        }
-      }
+      for (int ct = 0; ct < CT; ++ct)
+        if (valid[ct] && p == 3) st_granule(ho_r + 9 * N + 16 * ct + c, ho_tag, (uint32_t)action[ct]);
     }
     if (it == 0) SWARM_STAMP(5);
     // ---- env.step (VMAS World.step + scenario reward).  The 4 row groups of an agent

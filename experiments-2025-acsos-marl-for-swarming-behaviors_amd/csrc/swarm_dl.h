@@ -541,7 +541,11 @@ __device__ inline void dl_forward(const float* __restrict__ P, const DGeom<NS>& 
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       a0[t][0] = P[L_W + (16 * t + c) * kFeat + p];
-      a0[t][1] = (4 + p < kFeat) ? P[L_W + (16 * t + c) * kFeat + 4 + p] : 0.0f;
+      // read unconditionally (p = 3 reads the next row's first weight, inside the image) and
+      // masked after: no branch around a masked LDS read at the head of every forward
+      a0[t][1] = P[L_W + (16 * t + c) * kFeat + 4 + p];
+      asm volatile("" : "+v"(a0[t][1]));
+      a0[t][1] = (4 + p < kFeat) ? a0[t][1] : 0.0f;
     }
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)

@@ -121,14 +121,8 @@ struct TdFused {
 #ifndef SWARM_HO_FORCE_DROP
 #define SWARM_HO_FORCE_DROP 0
 #endif
-#ifndef SWARM_HO_PIPE
-#define SWARM_HO_PIPE 0   // A/B: two hand-off sweeps in flight (tools/ab_build.py); slower (r03)
-#endif
 #ifndef SWARM_HO_SLEEP
 #define SWARM_HO_SLEEP 1  // s_sleep argument (x 64 cycles) between two hand-off sweeps
-#endif
-#ifndef SWARM_HO_PREPOLL
-#define SWARM_HO_PREPOLL 0   // A/B: poll one granule per lane until it matches, then sweep all five
 #endif
 constexpr int kHoSpinLimit = SWARM_HO_SPIN_LIMIT;   // polls (with s_sleep) before a hand-off wait gives up
 // test builds only (libswarm_hip_hodrop.so): every hand-off wait overruns at once
@@ -270,13 +264,18 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     for (int ct = 0; ct < CT; ++ct)
       gid[ct] = n_graphs >= (uint32_t)S ? sample_index((uint32_t)min(sid[ct], S - 1), sk) : 0u;
   }
-  // fused: graphs of this tick's slot come from the acting waves' hand-off records
+  // graphs of this tick's slot (fused: they come from the acting waves' hand-off records).  A
+  // wave holding one takes the pre path in every kind of launch (fused, 3-launch, unfused), so
+  // the three stay bit-identical to each other
+  const uint32_t wslot = FUSED ? cc.write_slot : A.ctrl->write_slot;
   bool ho[CT];
-  bool wait = false;
+  bool wait = false, inslot = false;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
-    ho[ct] = FUSED && !SWARM_DIAG_NO_HO && live[ct] && n_graphs >= (uint32_t)S && gid[ct] / (uint32_t)B == cc.write_slot;
+    const bool cur = live[ct] && n_graphs >= (uint32_t)S && gid[ct] / (uint32_t)B == wslot;
+    ho[ct] = FUSED && !SWARM_DIAG_NO_HO && cur;
     wait = wait || ho[ct];
+    inslot = inslot || cur;
   }
   // replay rows written by earlier ticks: loads issued now (fused: every lane but the hand-off ones)
   float rew[CT];
@@ -308,6 +307,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   SWARM_STAMP(1);
   const bool waited = FUSED && __builtin_amdgcn_ballot_w64(wait) != 0;
+  // pre path: the online wave of a graph pair holding one of this tick's transitions forms its
+  // backward for gq = 1 before y (dZ, dT, dO, the attention scores' g and dp are linear in their
+  // target node's gq; the sums that mix targets, da_src and dh, stay after B2), in the time the
+  // block waits for the acting wave's s' and the target forward
+  const bool pre = online && __builtin_amdgcn_ballot_w64(inslot) != 0;
   bool live_drop[CT];   // this wave's graph was dropped after a hand-off overrun
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) live_drop[ct] = false;
@@ -318,96 +322,56 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     store_w_lds(Pon, R, threadIdx.x);
     if (pending && (cc.tick % (uint32_t)hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
     else ptg.store(Ptg, threadIdx.x);
-    // waves whose graphs wait for a hand-off are the tick's critical path: top issue priority
-    if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off):
-                    // online waves s and a, target waves s' (r is swept before y)
-      const uint32_t tag = cc.tick + 1u;
-      // one sweep: this lane's 5 granules of every hand-off graph slot (ct)
-      struct Sweep { unsigned long long g[CT][5]; };
-      auto issue = [&](Sweep& w) {
+  } else {
+    pon.store(Pon, threadIdx.x);
+    ptg.store(Ptg, threadIdx.x);
+  }
+  if (online && p == 0 && !waited) {
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          if (ho[ct]) {
-            const unsigned long long* rec = ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
-            const int j = min(jl[ct], N - 1);
-            const unsigned long long* sp = rec + (online ? 0 : 4 * N) + 4 * j;
-            w.g[ct][0] = ld_granule(sp); w.g[ct][1] = ld_granule(sp + 1); w.g[ct][2] = ld_granule(sp + 2);
-            w.g[ct][3] = ld_granule(sp + 3);
-            w.g[ct][4] = online ? ld_granule(rec + 9 * N + j) : ((unsigned long long)tag << 32);
-          }
-        }
-      };
-      // take a sweep's values; true when every tag of the wave matched
-      auto take = [&](const Sweep& w, bool (&okc)[CT]) -> bool {
-        bool ok = true;
+    for (int ct = 0; ct < CT; ++ct)
+      if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = act[ct];
+  }
+  __syncthreads();   // B0: weight images
+  SWARM_STAMP(2);
+  const uint32_t tag = cc.tick + 1u;
+  // granule address of this lane's node in a hand-off record: s at 0, s' at 4N, r at 8N, a at 9N
+  auto ho_at = [&](int ct, int off, int per_node) -> const unsigned long long* {
+    return ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) + off + per_node * min(jl[ct], N - 1);
+  };
+  if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off): online
+                  // waves s (published at the acting prologue), target waves s' (after the integrator).
+                  // Wave-local, after B0: the block's other waves are not held by it
+    for (int spin = 0;; ++spin) {
+      unsigned long long g[CT][4];
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          okc[ct] = true;
-          if (ho[ct]) {
-            okc[ct] = !kHoForceDrop && (uint32_t)(w.g[ct][0] >> 32) == tag && (uint32_t)(w.g[ct][1] >> 32) == tag &&
-                      (uint32_t)(w.g[ct][2] >> 32) == tag && (uint32_t)(w.g[ct][3] >> 32) == tag &&
-                      (uint32_t)(w.g[ct][4] >> 32) == tag;
-            ok = ok && okc[ct];
-            st[ct] = make_float4(__uint_as_float((uint32_t)w.g[ct][0]), __uint_as_float((uint32_t)w.g[ct][1]),
-                                 __uint_as_float((uint32_t)w.g[ct][2]), __uint_as_float((uint32_t)w.g[ct][3]));
-            if (online) act[ct] = nv[ct] ? (int)(uint32_t)w.g[ct][4] : 0;
-          }
-        }
-        return !__builtin_amdgcn_ballot_w64(!ok);
-      };
-#if SWARM_HO_PIPE
-      // two sweeps in flight: the next sweep's loads are issued before this one is checked, so a
-      // granule that lands between two sweeps is seen half a round trip sooner
-      Sweep sa, sb;
-      issue(sa);
-      for (int spin = 0;; spin += 2) {
-        bool okc[CT];
-        __builtin_amdgcn_s_sleep(1);
-        issue(sb);
-        if (take(sa, okc)) break;
-        if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
-          if (lane == 0) atomicAdd(X.ho_err, 1u);
-          drop_overrun<NS, GS>(okc, live_drop, nv, c);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        issue(sa);
-        if (take(sb, okc)) break;
-      }
-#else
-#if SWARM_HO_PREPOLL
-      // while the acting wave is still computing, poll only this lane's first granule of each
-      // hand-off slot (a fifth of the sweep's loads); the full sweep below then normally matches
-      // at once (the other four granules were stored beside it)
-      for (int spin = 0; spin < kHoSpinLimit; ++spin) {
-        bool ok = true;
+      for (int ct = 0; ct < CT; ++ct)
+        if (ho[ct]) {
+          const unsigned long long* sp = ho_at(ct, online ? 0 : 4 * N, 4);
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          if (ho[ct]) {
-            const unsigned long long* rec = ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N);
-            const unsigned long long g0 = ld_granule(rec + (online ? 0 : 4 * N) + 4 * min(jl[ct], N - 1));
-            ok = ok && (uint32_t)(g0 >> 32) == tag;
-          }
-        if (kHoForceDrop || !__builtin_amdgcn_ballot_w64(!ok)) break;
-        __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
-      }
-#endif
-      for (int spin = 0;; ++spin) {
-        Sweep sw;
-        bool okc[CT];
-        issue(sw);
-        if (take(sw, okc)) break;
-        if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
-          if (lane == 0) atomicAdd(X.ho_err, 1u);
-          drop_overrun<NS, GS>(okc, live_drop, nv, c);
-          break;
+          for (int k = 0; k < 4; ++k) g[ct][k] = ld_granule(sp + k);
         }
-        __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
+      bool ok = true, okc[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        okc[ct] = true;
+        if (ho[ct]) {
+          okc[ct] = !kHoForceDrop && (uint32_t)(g[ct][0] >> 32) == tag && (uint32_t)(g[ct][1] >> 32) == tag &&
+                    (uint32_t)(g[ct][2] >> 32) == tag && (uint32_t)(g[ct][3] >> 32) == tag;
+          ok = ok && okc[ct];
+          st[ct] = make_float4(__uint_as_float((uint32_t)g[ct][0]), __uint_as_float((uint32_t)g[ct][1]),
+                               __uint_as_float((uint32_t)g[ct][2]), __uint_as_float((uint32_t)g[ct][3]));
+        }
       }
-#endif
-      SWARM_RTSTAMP(10);
-      __builtin_amdgcn_s_setprio(3);
+      if (!__builtin_amdgcn_ballot_w64(!ok)) break;
+      if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
+        if (lane == 0) atomicAdd(X.ho_err, 1u);
+        drop_overrun<NS, GS>(okc, live_drop, nv, c);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
     }
+    SWARM_RTSTAMP(10);
+    __builtin_amdgcn_s_setprio(3);   // waves of hand-off graphs are the tick's critical path
   }
   DFwd<NS> F;
 #pragma unroll
@@ -415,35 +379,24 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     node_x(st[ct].x, st[ct].y, st[ct].z, st[ct].w, jl[ct], p, F.x[ct]);
     if (!nv[ct]) { F.x[ct][0] = 0.0f; F.x[ct][1] = 0.0f; }
   }
-  if (!FUSED) {
-    pon.store(Pon, threadIdx.x);
-    ptg.store(Ptg, threadIdx.x);
-  }
-  if (online && p == 0) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-      if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = act[ct];
-  }
-  __syncthreads();   // B0: weight images
-  SWARM_STAMP(2);
   // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121).
   //      Everything after B1 waits for the target waves' y, so they issue first.
   if (!online && !waited) __builtin_amdgcn_s_setprio(2);
   dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, A.radius, conv, nullptr, V, online, F);
-  if (FUSED && waited && !online) {   // r of this tick's transitions (published after the reward)
-    const uint32_t tag = cc.tick + 1u;
+  // fused: the rest of this tick's transitions, each as late as its first use: a for the online
+  // waves' pre path, r for the target waves' y (published after the acting wave's reward)
+  if (FUSED && waited) {
     for (int spin = 0;; ++spin) {
-      bool ok = true;
-      bool okc[CT];
+      bool ok = true, okc[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         okc[ct] = true;
         if (ho[ct] && !live_drop[ct]) {
-          const unsigned long long g = ld_granule(ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) +
-                                                  8 * N + min(jl[ct], N - 1));
+          const unsigned long long g = ld_granule(ho_at(ct, online ? 9 * N : 8 * N, 1));
           okc[ct] = !kHoForceDrop && (uint32_t)(g >> 32) == tag;
           ok = ok && okc[ct];
-          rew[ct] = __uint_as_float((uint32_t)g);
+          if (online) act[ct] = nv[ct] ? (int)(uint32_t)g : 0;
+          else rew[ct] = __uint_as_float((uint32_t)g);
         }
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
@@ -453,6 +406,107 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         break;
       }
       __builtin_amdgcn_s_sleep(1);
+    }
+    if (online && p == 0) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = nv[ct] ? act[ct] : 0;
+    }
+  }
+  // ---- pre path, before y: dZ1 = W2[a] * [z > 0], dO1 = (W1^T dZ1) (1 - t^2) (MFMA, as after B2),
+  //      g1 = H_u . dO1_v, dp1 / da_dst1 of the attention (scaled by gq after B1)
+  float dO1[CT][2][4], dp1[CT][CT][4], dad1[CT];
+  if (pre) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int ac = min(max(act[ct], 0), kActions - 1);
+      float dz1[2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float4 w = *reinterpret_cast<const float4*>(Pon + L_W2 + ac * kWRow + 16 * t + 4 * p);
+        float wv[4] = {w.x, w.y, w.z, w.w};
+        asm volatile("" : "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz1[t][r] = F.zr[ct][t][r] > 0.0f ? wv[r] : 0.0f;
+      }
+      float w1f[2][2][4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) w1f[t2][t][r] = Pon[L_W1 + (16 * t + 4 * p + r) * kWRow + 16 * t2 + c];
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) acc[t2] = mfma16(w1f[t2][t][r], dz1[t][r], acc[t2]);
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dO1[ct][t2][r] = acc[t2][r] * (1.0f - F.t[ct][t2][r] * F.t[ct][t2][r]);
+      dad1[ct] = 0.0f;
+#pragma unroll
+      for (int ut = 0; ut < CT; ++ut)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dp1[ct][ut][r] = 0.0f;
+    }
+    if (conv == SWARM_CONV_GAT) {
+      const WSmall<NS>& sm = *V.sm;
+      float ah[CT][2][4];
+#pragma unroll
+      for (int ut = 0; ut < CT; ++ut) {
+        const int u = min(16 * ut + c, NS - 1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float4 hv = *reinterpret_cast<const float4*>(&TB.H[row0 + u][16 * t + 4 * p]);
+          ah[ut][t][0] = hv.x; ah[ut][t][1] = hv.y; ah[ut][t][2] = hv.z; ah[ut][t][3] = hv.w;
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        float gv[CT][4], cu[CT][4];
+        float part = 0.0f;
+#pragma unroll
+        for (int ut = 0; ut < CT; ++ut) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc = mfma16(ah[ut][t][r], dO1[ct][t][r], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float cc4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int uq = 16 * ut + 4 * q + r;
+              cc4[q] = uq < NS ? F.cf[ct][uq < NS ? uq : 0] : 0.0f;
+            }
+            cu[ut][r] = p == 0 ? cc4[0] : (p == 1 ? cc4[1] : (p == 2 ? cc4[2] : cc4[3]));
+            gv[ut][r] = acc[r];
+            part = part + cu[ut][r] * gv[ut][r];
+          }
+        }
+        const float Gs = row4_sum(part);
+        float dsum = 0.0f;
+#pragma unroll
+        for (int ut = 0; ut < CT; ++ut)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = 16 * ut + 4 * p + r;
+            float dpu = 0.0f;
+            if (u < NS && cu[ut][r] != 0.0f) {   // in-edges only (cross-graph / absent: c = 0)
+              const float de = cu[ut][r] * (gv[ut][r] - Gs);
+              const float pre_act = sm.ssrc[u] + F.sdst[ct];
+              dpu = pre_act > 0.0f ? de : de * kLeakySlope;
+            }
+            dsum = dsum + dpu;
+            dp1[ct][ut][r] = dpu;
+          }
+        dad1[ct] = row4_sum(dsum);
+      }
     }
   }
   if (!online && p == 0) {
@@ -488,7 +542,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const float4 w = *reinterpret_cast<const float4*>(P + L_W2 + act[ct] * kWRow + 16 * t + 4 * p);
-        const float wv[4] = {w.x, w.y, w.z, w.w};
+        float wv[4] = {w.x, w.y, w.z, w.w};
+        asm volatile("" : "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]));   // one vector read, not 4 masked ones
 #pragma unroll
         for (int r = 0; r < 4; ++r) dz[ct][t][r] = F.zr[ct][t][r] > 0.0f ? wv[r] * gq : 0.0f;
       }
@@ -502,13 +557,39 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         for (int j = 0; j < NS / 4; ++j) TB.cm[row][4 * j + p] = pick4(F.cf[ct], j, p);
         if (p == 0) { TB.X[row][8] = 0.0f; TB.gq[row] = gq; TB.d2[row] = delta * delta; }
       }
+      if (pre) {   // the pre path's images scaled by this node's gq (rows free since B1)
+        float o[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[t][r] = nv[ct] ? dO1[ct][t][r] * gq : 0.0f;
+        if (n < NS) {
+          *reinterpret_cast<float4*>(&TB.dO[row0 + n][4 * p]) = make_float4(o[0][0], o[0][1], o[0][2], o[0][3]);
+          *reinterpret_cast<float4*>(&TB.dO[row0 + n][16 + 4 * p]) = make_float4(o[1][0], o[1][1], o[1][2], o[1][3]);
+          if (conv == SWARM_CONV_GAT) {
+#pragma unroll
+            for (int ut = 0; ut < CT; ++ut)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int u = 16 * ut + 4 * p + r;
+                if (u < NS) TB.dp[row0 + n][u] = nv[ct] ? dp1[ct][ut][r] * gq : 0.0f;
+              }
+          }
+        }
+        dad1[ct] = nv[ct] ? dad1[ct] * gq : 0.0f;
+      }
     }
   }
-  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph
+  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph (pre path: dO / dp too)
   SWARM_STAMP(5);
 
   const int col = lane & 31, h = lane >> 5;
   if (online) {
+    float da_d[CT];
+    WSmall<NS>& sm = *V.sm;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) da_d[ct] = pre ? dad1[ct] : 0.0f;
+    if (!pre) {
     // ---- dT^T = W1^T dZ^T on MFMA (the dz registers are the B operand),
     //      dO = dT * (1 - t^2) with the forward's tanh registers
     float dO[CT][2][4];
@@ -543,10 +624,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     SWARM_STAMP(24);
     // ---- GAT backward (attention part).  g[u][v] = H_u . dO_v on MFMA (A = H rows,
     //      B = the dO registers); lane (c, p) holds g[u = 16 ut + 4 p + r][v = 16 ct + c]
-    float da_d[CT];
-    WSmall<NS>& sm = *V.sm;
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) da_d[ct] = 0.0f;
     if (conv == SWARM_CONV_GAT) {
       float ah[CT][2][4];
 #pragma unroll
@@ -604,6 +681,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
     wave_lds_sync();   // dp / dO rows of this graph
+    }   // !pre
     SWARM_STAMP(25);
     // ---- dh_u = sum_v c[v][u] dO_v (MFMA: A = dO rows, B = C column) + da_src att_src + da_dst att_dst
     const float4 s0 = *reinterpret_cast<const float4*>(P + L_ATT_SRC + 4 * p);
@@ -623,9 +701,13 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       float da_s = 0.0f;
       if (conv == SWARM_CONV_GAT) {   // sum over the targets v of u's own graph
         const int base = (GS < NS) ? (uu / GS) * GS : 0;
+        float dpj[GS];   // read unconditionally (rows of this wave's graph), summed for j < N
 #pragma unroll
-        for (int j = 0; j < GS; ++j)
-          if (j < N) da_s = da_s + TB.dp[row0 + base + j][uu];
+        for (int j = 0; j < GS; ++j) dpj[j] = TB.dp[row0 + base + j][uu];
+#pragma unroll
+        for (int j = 0; j < GS; ++j) asm volatile("" : "+v"(dpj[j]));
+#pragma unroll
+        for (int j = 0; j < GS; ++j) da_s = j < N ? da_s + dpj[j] : da_s;
       }
       const float das = nv[ct] ? da_s : 0.0f, dad = nv[ct] ? da_d[ct] : 0.0f;
       f32x4 m0 = {0.f, 0.f, 0.f, 0.f}, m1 = {0.f, 0.f, 0.f, 0.f};
@@ -657,25 +739,45 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
         for (int r = 0; r < 16; ++r) sst(OFF_W1 + acc_row(r, h) * kHidden + col, dW1[r]);
       } else if (job == 1) {
-        f32x16 dW2 = {};
+        // every operand read up front: as `act == col ? gq : 0` the gq read became a branch
+        // around a masked load per step, an LDS round trip in front of each of the 16 MFMAs
+        int an[16];
+        float gn[16], rn[16];
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
           const int n = 2 * s + h;
-          const float a = (TB.act[n] == col) ? TB.gq[n] : 0.0f;
-          dW2 = mfma32(a, TB.R[n][col], dW2);
+          an[s] = TB.act[n];
+          gn[s] = TB.gq[n];
+          rn[s] = TB.R[n][col];
         }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(gn[s]));   // loaded unconditionally
+        f32x16 dW2 = {};
+#pragma unroll
+        for (int s = 0; s < 16; ++s) dW2 = mfma32(an[s] == col ? gn[s] : 0.0f, rn[s], dW2);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int a = acc_row(r, h);
           if (a < kActions) sst(OFF_W2 + a * kHidden + col, dW2[r]);
         }
-        if (lane < kActions || lane == 63) {   // every read issued before the ordered sum
-          float v[kTdRows];
+        if (lane < kActions || lane == 63) {   // the ordered sum over the 32 rows, 8 rows' reads at a time
+          // (each read unconditional: as selects around the reads they became a branch and an LDS
+          // round trip per row)
+          float acc = 0.0f;
 #pragma unroll
-          for (int n = 0; n < kTdRows; ++n) v[n] = lane == 63 ? TB.d2[n] : (TB.act[n] == lane ? TB.gq[n] : 0.0f);
-          float acc = v[0];
+          for (int k = 0; k < kTdRows; k += 8) {
+            int a8[8];
+            float g8[8], d8[8];
 #pragma unroll
-          for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+            for (int j = 0; j < 8; ++j) { a8[j] = TB.act[k + j]; g8[j] = TB.gq[k + j]; d8[j] = TB.d2[k + j]; }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(g8[j]), "+v"(d8[j]));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float v = lane == 63 ? d8[j] : (a8[j] == lane ? g8[j] : 0.0f);
+              acc = (k == 0 && j == 0) ? v : acc + v;
+            }
+          }
           sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
         }
       } else {
@@ -701,12 +803,18 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     for (int job = wall; job < 4; job += 2 * GPB) {
       if (job < 2) {
         const int t = job;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        // operands read up front and unconditionally (column 8 of X is +0: the padding columns
+        // c >= kFeat read it), so no LDS round trip sits between two MFMAs of the chain
+        float ha[kTdRows / 4], xb[kTdRows / 4];
 #pragma unroll
         for (int ks = 0; ks < kTdRows / 4; ++ks) {
           const int n = 4 * ks + p;
-          acc = mfma16(TB.dH[n][16 * t + c], c < kFeat ? TB.X[n][c] : 0.0f, acc);
+          ha[ks] = TB.dH[n][16 * t + c];
+          xb[ks] = TB.X[n][c < kFeat ? c : 8];
         }
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < kTdRows / 4; ++ks) acc = mfma16(ha[ks], xb[ks], acc);
         if (c < kFeat) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) sst(OFF_W + (16 * t + 4 * p + r) * kFeat + c, acc[r]);

@@ -55,14 +55,16 @@ def _rows(eng, idx):
 def _grad_bound_check(name, g_gpu, g32, g64):
     """Gradient, per parameter tensor: the GPU's largest distance to the float64 value is at most
     4x the fp32 oracle's own (torch autograd, the reference's arithmetic) plus 4 fp32 ulps of the
-    tensor's largest element; elementwise, every element is also within 1e-4 of its own magnitude
-    plus 2e-6 of the tensor's largest.  Gradient elements are sums over S*N nodes whose terms
+    tensor's largest element; elementwise, every element is also within 2e-4 of its own magnitude
+    plus 4e-6 of the tensor's largest (the fp32 oracle itself reaches 0.75 of half that bound on
+    conv1.att_dst, whose elements are softmax-backward sums that cancel to rounding noise, so a
+    tighter one would only test which of two valid fp32 summation orders got luckier).  Gradient elements are sums over S*N nodes whose terms
     cancel, so an element's rounding error scales with its terms, not with its value: both fp32
     paths sit thousands of ulps of the value away on such elements (profiles/
     r03_parity_errors_large.json), and an ulp bound on the value alone is meaningless there.
     Observed (round 3): GPU / oracle ratio <= 2.6 on every tensor of C2 and C3."""
     o = 0
-    worst, worst_ratio = 0.0, 0.0
+    worst, worst_ratio, worst_k = 0.0, 0.0, None
     for k, shape in O.PARAM_ORDER:
         n = 1
         for s in shape:
@@ -77,11 +79,15 @@ def _grad_bound_check(name, g_gpu, g32, g64):
         record(f"{name} grad[{k}] oracle32 vs fp64", st_o32, floor=floor)
         assert st_gpu["max_abs"] <= bound, (name, k, st_gpu["max_abs"], st_o32["max_abs"])
         worst_ratio = max(worst_ratio, st_gpu["max_abs"] / max(st_o32["max_abs"], 1e-30))
-        excess = ((a - b).abs() - (1e-4 * b.abs() + floor)).max().item()
-        worst = max(worst, excess)
+        elem_bound = 2e-4 * b.abs() + 2.0 * floor
+        excess = ((a - b).abs() - elem_bound).max().item()
+        record(f"{name} grad[{k}] elementwise: largest error / bound", {
+            "gpu": float(((a - b).abs() / elem_bound).max()), "oracle32": float(((c - b).abs() / elem_bound).max())})
+        if excess > worst:
+            worst, worst_k = excess, k
         o += n
     record(f"{name} grad: worst per-tensor ratio gpu/oracle32 error", {"ratio": worst_ratio})
-    assert worst <= 0.0, f"{name}: a gradient element outside 1e-4 rel + 2e-6 x tensor max (excess {worst:.3e})"
+    assert worst <= 0.0, f"{name}: a {worst_k} gradient element outside 2e-4 rel + 4e-6 x tensor max (excess {worst:.3e})"
 
 
 def _compare_update(name, eng, p0, t0, m0, v0, step0, idx, S, N):

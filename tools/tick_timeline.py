@@ -15,12 +15,15 @@ import torch  # noqa: E402
 
 import swarm_amd  # noqa: E402
 from swarm_amd import _lib  # noqa: E402
-from tools.stamps import ACT, ACT_ORDER, TD, report  # noqa: E402
+from tools.stamps import ACT, ACT_ORDER, TD, TD_ORDER, report  # noqa: E402
 
-# stamp 10 (granules matched) is a 100 MHz realtime stamp, reported in us above; the cycle
-# segments run from 1 straight to 2, i.e. the hand-off wait plus the B0 barrier
-TD_WAIT = {**TD, 2: "Adam + hand-off wait + B0 barrier"}
-TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 24, 25, 27, 6, 7]
+# stamp 10 (granules matched) is a 100 MHz realtime stamp, reported in us above.  The online
+# waves of hand-off graphs take the pre path (swarm_tdk.h): their s wait follows B0 and leads the
+# forward's first segment, their a wait and gq-free backward (dT, g, dp) come before y
+TD_WAIT = {**TD, 2: "Adam + B0 barrier", 16: "s hand-off wait + " + TD[16],
+           3: "a wait + pre path (dT, g MFMA, dp) + (y)", 5: "dQ/dZ + scaled dO/dp images + B2",
+           25: "(pre path: nothing)"}
+TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 25, 27, 6, 7]
 
 
 def main():
@@ -64,19 +67,28 @@ def main():
         for b in blocks_waiting[:12]:
             on = us(ho[b, :2][ho[b, :2] > 0])
             tg = us(ho[b, 2:][ho[b, 2:] > 0])
-            print(f"  TD block {b}: s/a matched {on.round(2).tolist()} us, s' matched {tg.round(2).tolist()} us, "
+            print(f"  TD block {b}: s matched {on.round(2).tolist()} us, s' matched {tg.round(2).tolist()} us, "
                   f"block end {us(td[b, :, 9].max()):.2f} us")
+        other = np.setdiff1d(np.arange(td.shape[0]), blocks_waiting)
+        oe = us(td[other][..., 9][td[other][..., 9] > 0])
+        print(f"  TD blocks without hand-offs: waves end p50 {np.median(oe):.2f} p99 {np.percentile(oe, 99):.2f} "
+              f"max {oe.max():.2f} us")
         nw = te[te > np.percentile(te, 99)]
         print(f"  slowest 1% TD waves end at {np.sort(nw).round(2).tolist()[-6:]} us")
         if rep == 2:   # per-segment medians (s_memtime cycles) of the critical waves
             print("  acting waves:")
             report(act.reshape(-1), ACT, act.shape[0] * 4, ACT_ORDER)
-            wv = td.reshape(-1, 32)
-            wv = wv[wv[:, 10] > 0]
-            wv = wv[wv[:, 24] > 0]   # online waves of waiting graphs
+            wv = td[:, :2].reshape(-1, 32)   # online waves (2 per block at N <= 8)
+            wv = wv[wv[:, 10] > 0]            # ... of waiting graphs
             if len(wv):
                 print(f"  online TD waves of hand-off graphs ({len(wv)}):")
                 report(wv.reshape(-1), TD_WAIT, len(wv), TD_WAIT_ORDER)
+            tv = td[:, 2:].reshape(-1, 32)   # target waves of blocks with hand-off graphs
+            tv = tv[tv[:, 10] > 0]
+            if len(tv):
+                print(f"  target TD waves of hand-off graphs ({len(tv)}):")
+                report(tv.reshape(-1), {**TD, 2: "Adam + B0 barrier", 16: "s' hand-off wait + " + TD[16],
+                                        3: "r wait + (y)"}, len(tv), TD_ORDER)
 
 
 if __name__ == "__main__":
