@@ -52,6 +52,7 @@ struct TdLds {
   float y[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];
   int act[kTdRows];
   int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
+  int prew[GPB];                  // online wave w is on the pre path (swarm_tdk.h td_body)
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
   __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
 };
@@ -522,6 +523,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     }
   }
   if (!online && !waited) __builtin_amdgcn_s_setprio(0);
+  if (online && lane == 0) TB.prew[wi] = pre ? 1 : 0;
   SWARM_STAMP(3);
   __syncthreads();   // B1: TD targets
   SWARM_STAMP(4);
@@ -582,6 +584,69 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph (pre path: dO / dp too)
   SWARM_STAMP(5);
+  int np_pre = 0;   // online waves of this block on the pre path
+#pragma unroll
+  for (int w2 = 0; w2 < GPB; ++w2) np_pre += TB.prew[w2];
+  // the parameter products that need only B2's images (each writes its slice of the slab)
+  auto b2_job = [&](int job) {
+    const int col = lane & 31, h = lane >> 5;
+    if (job == 0) {
+      const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sst(OFF_W1 + acc_row(r, h) * kHidden + col, dW1[r]);
+    } else if (job == 1) {
+      // every operand read up front: as `act == col ? gq : 0` the gq read became a branch
+      // around a masked load per step, an LDS round trip in front of each of the 16 MFMAs
+      int an[16];
+      float gn[16], rn[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int n = 2 * s + h;
+        an[s] = TB.act[n];
+        gn[s] = TB.gq[n];
+        rn[s] = TB.R[n][col];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(gn[s]));   // loaded unconditionally
+      f32x16 dW2 = {};
+#pragma unroll
+      for (int s = 0; s < 16; ++s) dW2 = mfma32(an[s] == col ? gn[s] : 0.0f, rn[s], dW2);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int a = acc_row(r, h);
+        if (a < kActions) sst(OFF_W2 + a * kHidden + col, dW2[r]);
+      }
+    } else if (job == 2) {
+      if (lane < kHidden) {
+        float v[kTdRows];
+#pragma unroll
+        for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        sst(OFF_B1 + lane, acc);
+      }
+    } else if (lane < kActions || lane == 63) {   // db2 / loss: the ordered sum over the 32 rows,
+      // 8 rows' reads at a time (each read unconditional: as selects around the reads they became
+      // a branch and an LDS round trip per row)
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kTdRows; k += 8) {
+        int a8[8];
+        float g8[8], d8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a8[j] = TB.act[k + j]; g8[j] = TB.gq[k + j]; d8[j] = TB.d2[k + j]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(g8[j]), "+v"(d8[j]));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = lane == 63 ? d8[j] : (a8[j] == lane ? g8[j] : 0.0f);
+          acc = (k == 0 && j == 0) ? v : acc + v;
+        }
+      }
+      sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
+    }
+  };
 
   const int col = lane & 31, h = lane >> 5;
   if (online) {
@@ -732,66 +797,15 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     SWARM_STAMP(27);
   } else {
     // ---- target waves: products that need only B2's images
-    //      job 0: dW1 = dZ^T T ; job 1: dW2 = onehot(a) gq R, db2, loss ; job 2: db1
-    for (int job = wi; job < 3; job += GPB) {
-      if (job == 0) {
-        const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sst(OFF_W1 + acc_row(r, h) * kHidden + col, dW1[r]);
-      } else if (job == 1) {
-        // every operand read up front: as `act == col ? gq : 0` the gq read became a branch
-        // around a masked load per step, an LDS round trip in front of each of the 16 MFMAs
-        int an[16];
-        float gn[16], rn[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int n = 2 * s + h;
-          an[s] = TB.act[n];
-          gn[s] = TB.gq[n];
-          rn[s] = TB.R[n][col];
-        }
-#pragma unroll
-        for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(gn[s]));   // loaded unconditionally
-        f32x16 dW2 = {};
-#pragma unroll
-        for (int s = 0; s < 16; ++s) dW2 = mfma32(an[s] == col ? gn[s] : 0.0f, rn[s], dW2);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int a = acc_row(r, h);
-          if (a < kActions) sst(OFF_W2 + a * kHidden + col, dW2[r]);
-        }
-        if (lane < kActions || lane == 63) {   // the ordered sum over the 32 rows, 8 rows' reads at a time
-          // (each read unconditional: as selects around the reads they became a branch and an LDS
-          // round trip per row)
-          float acc = 0.0f;
-#pragma unroll
-          for (int k = 0; k < kTdRows; k += 8) {
-            int a8[8];
-            float g8[8], d8[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { a8[j] = TB.act[k + j]; g8[j] = TB.gq[k + j]; d8[j] = TB.d2[k + j]; }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(g8[j]), "+v"(d8[j]));
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float v = lane == 63 ? d8[j] : (a8[j] == lane ? g8[j] : 0.0f);
-              acc = (k == 0 && j == 0) ? v : acc + v;
-            }
-          }
-          sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
-        }
-      } else {
-        if (lane < kHidden) {
-          float v[kTdRows];
-#pragma unroll
-          for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
-          float acc = v[0];
-#pragma unroll
-          for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-          sst(OFF_B1 + lane, acc);
-        }
-      }
-    }
+    //      job 0: dW1 = dZ^T T ; job 1: dW2 = onehot(a) gq R ; job 2: db1 ; job 3: db2, loss.
+    //      The vector sums (2, 3) go to the block's pre-path online waves when it has any: theirs
+    //      is the short side of B2 -> B3 there, and the target waves' products the long one
+    for (int job = wi; job < 4; job += GPB)
+      if (job < 2 || np_pre == 0) b2_job(job);
+  }
+  if (online && pre) {   // (GPB = 2: one pre wave takes both sums, two split them)
+    if (np_pre == 1 || wi == 0) b2_job(2);
+    if (np_pre == 1 || wi == 1) b2_job(3);
   }
   __syncthreads();   // B3: dO / dH / das / dad
   SWARM_STAMP(6);

@@ -6,9 +6,9 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED" gpurun_out/pytest_gpu.log | head -30; exit $rc; fi
-VARIANTS="base old" REPS=${REPS:-3} bash scripts/ab_bench.sh > /dev/null || exit $?
+VARIANTS="${VARIANTS:-base old}" REPS=${REPS:-3} bash scripts/ab_bench.sh > /dev/null || exit $?
 cp gpurun_out/ab.jsonl gpurun_out/ab_c2.jsonl; cat gpurun_out/ab_c2.jsonl | cut -c1-200
-VARIANTS="base old" REPS=2 BENCH_ARGS="--scenario ObstacleAvoidance --agents 12" bash scripts/ab_bench.sh > /dev/null || exit $?
+VARIANTS="${VARIANTS:-base old}" REPS=2 BENCH_ARGS="--scenario ObstacleAvoidance --agents 12" bash scripts/ab_bench.sh > /dev/null || exit $?
 cp gpurun_out/ab.jsonl gpurun_out/ab_c3.jsonl; cat gpurun_out/ab_c3.jsonl | cut -c1-200
 if [ -n "$TIMELINE" ]; then
   timeout -k 10 300 python tools/tick_timeline.py > gpurun_out/timeline.txt 2>&1 || exit $?
