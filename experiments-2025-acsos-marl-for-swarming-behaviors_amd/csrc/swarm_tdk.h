@@ -86,11 +86,17 @@ __device__ inline void slab_st(float* p, float v) {
 }
 
 // D[i][j] = sum_node A_img[node][i] * B_img[node][j] over the 32 node rows (MFMA, K = node)
+// (all 32 operands read first: no LDS round trip between two steps of the MFMA chain)
 __device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*Bimg)[kRow], int lane) {
-  f32x16 acc = {};
   const int h = lane >> 5, c = lane & 31;
+  float a[16], b[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma32(Aimg[2 * s + h][c], Bimg[2 * s + h][c], acc);
+  for (int s = 0; s < 16; ++s) { a[s] = Aimg[2 * s + h][c]; b[s] = Bimg[2 * s + h][c]; }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(a[s]), "+v"(b[s]));
+  f32x16 acc = {};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(a[s], b[s], acc);
   return acc;
 }
 
