@@ -813,6 +813,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     if (np_pre == 1 || wi == 0) b2_job(2);
     if (np_pre == 1 || wi == 1) b2_job(3);
   }
+  SWARM_STAMP(26);   // stamps build: the B2 jobs done, before the B3 wait
   __syncthreads();   // B3: dO / dH / das / dad
   SWARM_STAMP(6);
   // ---- products over B3's images, spread over all 2 GPB waves of the block:

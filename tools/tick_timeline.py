@@ -22,8 +22,8 @@ from tools.stamps import ACT, ACT_ORDER, TD, TD_ORDER, report  # noqa: E402
 # forward's first segment, their a wait and gq-free backward (dT, g, dp) come before y
 TD_WAIT = {**TD, 2: "Adam + B0 barrier", 16: "s hand-off wait + " + TD[16],
            3: "a wait + pre path (dT, g MFMA, dp) + (y)", 5: "dQ/dZ + scaled dO/dp images + B2",
-           25: "(pre path: nothing)"}
-TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 25, 27, 6, 7]
+           25: "(pre path: nothing)", 26: "B2 jobs (pre online: vector sums)", 6: "B3 barrier wait"}
+TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 25, 27, 26, 6, 7]
 
 
 def main():
@@ -88,7 +88,9 @@ def main():
             if len(tv):
                 print(f"  target TD waves of hand-off graphs ({len(tv)}):")
                 report(tv.reshape(-1), {**TD, 2: "Adam + B0 barrier", 16: "s' hand-off wait + " + TD[16],
-                                        3: "r wait + (y)"}, len(tv), TD_ORDER)
+                                        3: "r wait + (y)", 26: "B2 jobs (dW1 / dW2 MFMA products)",
+                                        6: "B3 barrier wait"},
+                       len(tv), [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 26, 6, 7])
 
 
 if __name__ == "__main__":
