@@ -14,15 +14,21 @@ the per-episode times (HIP events between steps).  Inputs: synthetic reset state
 pre-filled with 100 acting ticks.  Each episode's 100 ticks replay one captured hipGraph.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+       N > 1 under a launcher (torch.distributed.run --nproc-per-node N ... bench.py --gpus N): one
+       rank per process as the launcher started them.  N > 1 without one (WORLD_SIZE unset): this
+       process starts the N ranks itself (a torch.distributed.run child, before any GPU call), relays
+       their output and exits non-zero if a rank fails or the JSON line's n_gpus is not N.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -130,13 +136,71 @@ def parse():
     return ap.parse_args()
 
 
+def launch_decision(gpus: int, env) -> str:
+    """How this process runs --gpus N: "run" (one rank: N == 1, or a launcher set WORLD_SIZE == N)
+    or "spawn" (N > 1 and no launcher: start the N ranks first).  A launcher's WORLD_SIZE that
+    differs from N is an error (SystemExit): the line would be quoted for the wrong GPU count."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={ws}")
+    return "run"
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(argv, n: int, port: int, script: str = None):
+    """torch.distributed.run command that starts n ranks of this script with the same arguments
+    (one node, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(argv, n: int, script: str = None) -> int:
+    """Start n ranks as a child process (never an exec: this process has not touched the GPU and
+    stays the parent), relay their stdout line by line, and return non-zero if the launcher fails
+    or rank 0's JSON line does not report n GPUs."""
+    cmd = rank_launch_cmd(argv, n, free_port(), script)
+    print("[bench] starting %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for raw in proc.stdout:
+        sys.stdout.write(raw)
+        sys.stdout.flush()
+        if raw.lstrip().startswith("{"):
+            try:
+                d = json.loads(raw)
+            except ValueError:
+                continue
+            if "n_gpus" in d:
+                line = d
+    rc = proc.wait()
+    if rc != 0:
+        print(f"[bench] rank launcher exited with {rc}", file=sys.stderr)
+        return rc
+    if line is None or line.get("n_gpus") != n:
+        print(f"[bench] expected a JSON line with n_gpus {n}, got {None if line is None else line.get('n_gpus')}",
+              file=sys.stderr)
+        return 3
+    return 0
+
+
 def main():
     args = parse()
+    if launch_decision(args.gpus, os.environ) == "spawn":
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world != args.gpus:   # launch_decision guarantees it; kept as the invariant the line relies on
+        raise SystemExit(f"--gpus {args.gpus} but world size {world}")
     torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))   # several gloo ranks may share a GPU
     distributed = world > 1 or args.force_dist
     import swarm_amd
@@ -148,6 +212,7 @@ def main():
     if distributed:
         torch.distributed.barrier()
 
+    build = lib_identity()
     peer, allreduce = None, None
     if distributed and args.mode == "train":
         allreduce = "rccl" if args.backend == "nccl" else args.backend
@@ -307,13 +372,14 @@ def main():
     ms = elapsed / args.steps * 1e3          # per step (episode)
     tick_ms = ms / max_steps
 
-    # ---- per-kernel durations.  Fused tick: a captured chain of KCHAIN real tick launches, each
-    #      followed by swarm_ctrl_advance (tick counter, replay slot: every launch publishes and
-    #      waits on fresh hand-off stamps, as in the timed ticks), HIP events recorded on the
-    #      stream the graph launches on; the advance launch's own duration (a chain of it alone)
-    #      is subtracted.  The slab reduce's share of a tick is the tick time minus that.
-    #      3-launch tick: each kernel as a captured chain of KCHAIN back-to-back launches (TD
-    #      and the slab reduce are pure functions of their inputs).
+    # ---- per-kernel durations, each as the period of a captured chain of real launches timed with
+    #      HIP events on the stream the graph launches on (a period holds the kernel and one launch
+    #      boundary).  Fused tick: tick_kernel = period of (tick launch, swarm_ctrl_advance) pairs
+    #      minus the period of the advance alone (every tick launch advances the tick counter and the
+    #      replay slot, so its hand-off waits are real); reduce_advance = period of the slab reduce
+    #      alone; tick_period = period of whole ticks (tick launch + reduce), the tick without the
+    #      timed region's per-episode reset.  3-launch tick: each kernel's chain (TD and the slab
+    #      reduce are pure functions of their inputs).
     kt = {}
     if not args.no_kernel_timing:
         stream = torch.cuda.current_stream()
@@ -331,23 +397,17 @@ def main():
                 per.append(e0.elapsed_time(e1) * 1e3 / kchain)
             return float(np.median(per))   # microseconds per launch
 
-        if fused and eng.tick_reduce:
-            # one launch per tick: the slab reduce and the ctrl advance run inside the tick kernel
-            eng.reset()
-            kt["tick_kernel"] = chain_us(eng.launch_tick, 40)
-            kt["ctrl_advance_kernel (an empty launch's period, for scale)"] = chain_us(eng.advance, 40)
-            eng.flush()
-            eng.reset()
-            assert eng.handoff_errors() == 0, "fused tick: a hand-off or reduce wait hit its bound"
-        elif fused:
+        if fused:
             eng.reset()
             t_pair = chain_us(lambda: (eng.launch_tick(), eng.advance()), 40)
             t_adv = chain_us(eng.advance, 40)
+            kt["tick_kernel"] = t_pair - t_adv
+            kt["ctrl_advance_kernel (an empty launch's period)"] = t_adv
+            if eng.peer is None and world == 1:
+                kt["reduce_advance (period)"] = chain_us(eng.launch_reduce_advance, 40)
+                kt["tick_period (tick + reduce)"] = chain_us(lambda: (eng.launch_tick(), eng.launch_reduce_advance()), 40)
             eng.flush()
             eng.reset()
-            kt["tick_kernel"] = t_pair - t_adv
-            kt["ctrl_advance_kernel"] = t_adv
-            kt["grad_reduce_kernel (tick share)"] = tick_ms * 1e3 - kt["tick_kernel"]
             assert eng.handoff_errors() == 0, "fused tick: a hand-off wait hit its bound"
         else:
             for name, fn in (("td_kernel", eng.launch_td), ("act_kernel", eng.launch_train_act),
@@ -367,24 +427,24 @@ def main():
         if fused:   # the dominant kernel is the whole fused tick kernel (acting + TD blocks)
             t_k = kt["tick_kernel"] * 1e-6
             flops, nbytes = act_flops_launch + td_flops_launch, B * N * 69 + S * N * 37
-            kname, pmcf = "tick_kernel (swarm_train_tick: acting + TD blocks)", "r01_pmc_tick.json"
+            kname, pmcf = "tick_kernel (swarm_train_tick: acting + TD blocks)", "tick"
         else:
             t_k = kt["td_kernel"] * 1e-6
             flops, nbytes = td_flops_launch, S * N * 37
-            kname, pmcf = "td_kernel (swarm_td_grad)", "r01_pmc_td.json"
+            kname, pmcf = "td_kernel (swarm_td_grad)", "td"
         ach = flops / t_k / 1e12
         traffic, mfma_util, pmc_src = None, None, None
-        for rnd in ("r03_", "r02_", "r01_"):   # the newest round's PMC passes (scripts/pmc.sh)
-            pmc = os.path.join(ROOT, "profiles", pmcf.replace("r01_", rnd))
-            if os.path.exists(pmc) and headline:
-                d = json.load(open(pmc))
-                traffic = d.get("hbm_bytes_per_launch")
-                kk = d.get("kernels", {}).get(d.get("kernel", ""), {}).get("counters", {})
+        if headline:   # counters only from a profile of THIS library build (tools/pmc_summary.py)
+            pmc_src = find_pmc(pmcf, build)
+            if pmc_src.get("file"):
+                dd = pmc_src.pop("data")
+                traffic = dd.get("hbm_bytes_per_launch")
+                kk = dd.get("kernels", {}).get(dd.get("kernel", ""), {}).get("counters", {})
                 busy = kk.get("SQ_VALU_MFMA_BUSY_CYCLES")
                 if busy is not None:   # MFMA pipe cycles / (1024 SIMDs x this launch's time at the 2.4 GHz peak clock)
                     mfma_util = busy / (1024 * PEAK_CLOCK_GHZ * 1e9 * t_k)
-                pmc_src = os.path.basename(pmc)
-                break
+        else:
+            pmc_src = {"file": None, "reason": "counters are collected for the headline configuration only"}
         roof = {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
                 "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic, "kernel": kname,
@@ -433,15 +493,44 @@ def main():
                            "parallelism": f"env-sharded dp{world}" + ("" if not distributed else
                                           " + xGMI peer grad all-reduce" if peer is not None else
                                           f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce"),
-                           "hipgraph": graph is not None, "tick": ("1 launch (slab reduce + ctrl advance in-kernel)" if fused and eng.tick_reduce else
-                                    "1 launch + reduce" if fused else "3 launches"),
+                           "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
                            "allreduce": allreduce, "allreduce_paths": both, "rank_errors": rank_errors,
                            "replicas_identical": replicas},
-                "roofline": roof, "cpu_baseline": cpu, "acting_only": acting,
+                "roofline": roof, "cpu_baseline": cpu, "acting_only": acting, "build": build,
                 "loss": ctrl["loss"]}
         print(json.dumps(line))
     if distributed:
         torch.distributed.destroy_process_group()
+
+
+def lib_identity() -> dict:
+    """The library this process runs: swarm_build_info() (ABI, source digest) and the .so's sha256."""
+    from swarm_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return {"info": _lib.load().swarm_build_info().decode(), "lib_sha256": h.hexdigest()}
+
+
+def find_pmc(kernel: str, build: dict) -> dict:
+    """The newest PMC summary under profiles/ (tools/pmc_summary.py) for `kernel` whose recorded
+    build is this library (same swarm_build_info, i.e. the same sources and flags); none -> the
+    reason, and the roofline's counters stay null."""
+    cands = []
+    for f in os.listdir(os.path.join(ROOT, "profiles")):
+        if f.endswith(".json") and "pmc" in f:
+            try:
+                d = json.load(open(os.path.join(ROOT, "profiles", f)))
+            except ValueError:
+                continue
+            if isinstance(d, dict) and d.get("kernel") == kernel:
+                cands.append((os.path.getmtime(os.path.join(ROOT, "profiles", f)), f, d))
+    for _, f, d in sorted(cands, reverse=True):
+        b = d.get("build") or {}
+        if b.get("info") == build["info"]:
+            return {"file": f, "match": "build_info" + (" + lib_sha256" if b.get("lib_sha256") == build["lib_sha256"]
+                                                       else ""), "data": d}
+    return {"file": None, "reason": f"no PMC summary of this build ({build['info']}) under profiles/"}
 
 
 def host_cpu():

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SWARM_LIB_PATH") or os.path.join(HERE, "libswarm_hip.
 SWARM_GOTO, SWARM_OBSTACLE_AVOIDANCE, SWARM_FLOCKING = 0, 1, 2
 GRAPH_COMPLETE, GRAPH_KNN, GRAPH_DENSE, GRAPH_RADIUS = 0, 1, 2, 3
 CONV_GAT, CONV_GCN = 0, 1
-F_SHARED_RESET, F_RANDOM_OA, F_TICK_REDUCE = 1, 2, 4
+F_SHARED_RESET, F_RANDOM_OA = 1, 2
 N_PARAMS = 1673
 NET_GCN, NET_GAT3 = 0, 1
 GAT3_N_PARAMS = 409
@@ -26,7 +26,7 @@ ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
           -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class SwarmConfig(ctypes.Structure):
@@ -104,7 +104,6 @@ _PROTOS = {
     "swarm_host_topk_set": (c_int32, [POINTER(c_float), c_int32, c_int32, POINTER(ctypes.c_uint8)]),
     "swarm_train_tick_supported": (c_int32, [POINTER(SwarmConfig)]),
     "swarm_train_tick_workspace_bytes": (c_int64, [POINTER(SwarmConfig)]),
-    "swarm_train_tick_reduce_supported": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg)]),
     "swarm_train_tick": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
                                    POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p, c_void_p,
                                    c_void_p, c_void_p]),

@@ -2,6 +2,7 @@
 travels with the repository snapshot to the GPU box)."""
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -25,6 +26,18 @@ def _deps():
     files += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h") and f not in HEADERS]
     files.append(os.path.join(os.path.dirname(HERE), "include", "swarm_hip.h"))
     return files
+
+
+def source_digest(extra=()) -> str:
+    """sha256 (16 hex digits) of every source, header and compiler flag of a build: compiled into
+    the library (swarm_build_info) so that a profile can name the code it measured."""
+    h = hashlib.sha256()
+    for f in sorted(_deps()):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS + list(extra)).encode())
+    return h.hexdigest()[:16]
 
 
 def up_to_date() -> bool:
@@ -53,7 +66,7 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False, varia
         return out
     # one hipcc process per translation unit (in parallel), then one link
     objs = [f"{out}.{os.path.splitext(src)[0]}.o" for src in SOURCES]
-    cflags = [f for f in FLAGS if f != "-shared"]
+    cflags = [f for f in FLAGS if f != "-shared"] + [f'-DSWARM_SRC_DIGEST="{source_digest(extra)}"']
     procs = []
     for src, obj in zip(SOURCES, objs):
         cmd = [HIPCC, *cflags, *extra, "-c", "-o", obj, os.path.join(CSRC, src)]

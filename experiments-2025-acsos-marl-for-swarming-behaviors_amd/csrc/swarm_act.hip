@@ -246,7 +246,24 @@ extern "C" {
 
 int swarm_abi_version(void) { return SWARM_ABI_VERSION; }
 int swarm_n_params(void) { return N_PARAMS; }
-const char* swarm_build_info(void) { return "libswarm_hip gfx950 (wave-per-graph VALU forward, MFMA f32 32x32x2 weight-gradient products, wave64)"; }
+#ifndef SWARM_SRC_DIGEST
+#define SWARM_SRC_DIGEST "unknown"
+#endif
+#define SWARM_STR2(x) #x
+#define SWARM_STR(x) SWARM_STR2(x)
+// the build's identity: ABI, the source digest build.py computes over every source, header and
+// flag, and the variant knobs; profiles record it (tools/pmc_summary.py) and bench.py uses a
+// profile's counters only for the library that wrote them
+const char* swarm_build_info(void) {
+  return "libswarm_hip gfx950 abi " SWARM_STR(SWARM_ABI_VERSION) " src " SWARM_SRC_DIGEST
+#if SWARM_STAMPS
+         " stamps"
+#endif
+#if SWARM_HO_FORCE_DROP
+         " hodrop"
+#endif
+      ;
+}
 
 int swarm_env_reset(const swarm_config* cfg, float* state, uint32_t episode, void* stream) {
   if (int e = check_cfg(cfg)) return e;
@@ -343,8 +360,7 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
   if (cfg->net != SWARM_NET_GCN) return SWARM_E_UNSUPPORTED;   // GAT3: forward only
   ActArgs a = make_args(cfg);
   a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = sample_out;
-  static const bool no_gn = getenv("SWARM_NO_GN") != nullptr;   // A/B knob (diagnostics)
-  a.grad_norm_out = no_gn ? nullptr : const_cast<float*>(&ctrl->grad_norm);
+  a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
   if (replay) a.replay = *replay;
   if (out) a.out = *out;
   return launch_act<MODE_TICK>(a, n_tiles(cfg), (hipStream_t)stream);
@@ -361,18 +377,6 @@ int swarm_rollout(const swarm_config* cfg, const float* params, float* state, in
   return launch_act<MODE_ROLLOUT>(a, n_tiles(cfg), (hipStream_t)stream);
 }
 
-#if SWARM_DIAG_TIE_COUNT
-// diagnostic library only: {kNN builds (waves x ticks), builds with a tie row, tie rows} since load
-int swarm_dbg_tie_counts(unsigned long long* out3) {
-  hipError_t e = hipMemcpyFromSymbol(&out3[0], HIP_SYMBOL(g_swarm_knn_calls), 8);
-  if (e == hipSuccess) e = hipMemcpyFromSymbol(&out3[1], HIP_SYMBOL(g_swarm_tie_calls), 8);
-  if (e == hipSuccess) e = hipMemcpyFromSymbol(&out3[2], HIP_SYMBOL(g_swarm_tie_rows), 8);
-  return (int)e;
-}
-int swarm_dbg_tie_env(unsigned int* out4096) {
-  return (int)hipMemcpyFromSymbol(out4096, HIP_SYMBOL(g_swarm_tie_env), 4096 * 4);
-}
-#endif
 #if SWARM_STAMPS
 int swarm_dbg_stamps_act(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_swarm_stamps), &p, sizeof(p)); }
 #endif

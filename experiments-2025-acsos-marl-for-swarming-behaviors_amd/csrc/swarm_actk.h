@@ -38,7 +38,6 @@ struct ActArgs {
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
   int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
   unsigned long long* ho_rec;   // fused tick: [B][ho_stride_granules(N)] hand-off records (swarm_common.h)
-  unsigned long long* red_ws;   // one-launch tick (swarm_red.h): the workspace's counter words
 };
 
 constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
@@ -64,8 +63,7 @@ struct ActSmem {
 // training-tick kernel runs acting blocks beside TD blocks).
 // HO: fused-tick hand-off publishing (swarm_tick.hip only).  NET: SWARM_NET_GCN (the D-layout
 // MFMA forward) or SWARM_NET_GAT3 (swarm_gat3.h; acting only, no learner prologue)
-// RED: one-launch tick (swarm_red.h): the block counts itself past its prologue
-template <int NS, int MODE, int SCEN, int SPEC, bool HO = false, int NET = SWARM_NET_GCN, bool RED = false>
+template <int NS, int MODE, int SCEN, int SPEC, bool HO = false, int NET = SWARM_NET_GCN>
 __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int nvb,
                                          const swarm_ctrl* __restrict__ ctrl, float* state, const float* grad,
                                          const float* w_cur, const float* m_cur, const float* v_cur, int B, int N,
@@ -132,8 +130,6 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // flight together instead of dependent loads behind branches)
   swarm_ctrl cc = {};
   if (MODE == MODE_TICK) cc = *ctrl;
-  unsigned long long red_epoch = 0ull;   // RED: this launch's epoch, with ctrl's round trip
-  if constexpr (RED) red_epoch = red_epoch_load(A.red_ws);
   uint32_t tick = A.tick0;
   float eps = A.eps;
   uint32_t slot = 0;
@@ -149,7 +145,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // fused tick: is this env's transition in the TD batch drawn from this tick's slot?
   // (position of graph id slot * B + env in the keyed permutation < batch)
   bool ho_pub = false;
-  if (MODE == MODE_TICK && HO && d.live && !SWARM_DIAG_NO_HO) {
+  if (MODE == MODE_TICK && HO && d.live) {
     const uint32_t cap = (uint32_t)A.replay.capacity;
     const uint32_t filled = cc.filled_slots;
     const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)B;
@@ -158,8 +154,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       ho_pub = sample_position(slot * (uint32_t)B + (uint32_t)d.gid, sk) < (uint32_t)A.hp.batch;
     }
   }
-  // the late stores' pointers fetched from the kernarg segment now, beside the wait
-  // explore0 already has, and pinned in SGPRs: no kernarg round trip later in the wave
+  // the late stores' pointers, fetched from the kernarg segment beside the wait explore0
+  // already has
   float* rp_s = A.replay.s;
   float* rp_sn = A.replay.s_next;
   float* rp_r = A.replay.r;
@@ -168,9 +164,6 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   float* o_avg = A.out.avg_dist;
   float* o_hits = A.out.hits;
   int32_t* smp = A.sample_out;
-#if SWARM_PIN
-  asm volatile("" : "+s"(rp_s), "+s"(rp_sn), "+s"(rp_r), "+s"(rp_a), "+s"(o_rew), "+s"(o_avg), "+s"(o_hits), "+s"(smp));
-#endif
   // fused tick: s of a sampled transition is the state loaded above, so it is published now, a
   // whole optimizer step and forward ahead of a: the waiting online TD wave runs its forward on
   // s (and its gq-free backward once a lands) while this wave computes (swarm_tdk.h, pre path)
@@ -212,14 +205,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     ps.store(Pw, threadIdx.x);
   }
   __syncthreads();   // weight image complete
-  if constexpr (RED) {   // ctrl, grad and _cur are read (block 0's _nxt stores are its own, swarm_red.h)
-    if (threadIdx.x == 0) red_count(A.red_ws + kWsActPro, red_epoch);
-  }
   const float* P = Pw;
   SWARM_STAMP(1);
-#if SWARM_DIAG_ACT   // diagnostic A/B builds only: acting waves stop after the optimizer step
-  if (MODE == MODE_TICK && HO && (SWARM_DIAG_ACT == 2 || (w & 1))) return;
-#endif
 
   const int n_ticks = (MODE == MODE_ROLLOUT) ? A.n_ticks : 1;
   float rew_sum[CT], hits_sum = 0.0f;

@@ -12,14 +12,6 @@
 
 #include "../../include/swarm_hip.h"
 
-// diagnostic A/B knobs (tools/ab_build.py only; 0 in every shipped library)
-#ifndef SWARM_DIAG_NO_HO
-#define SWARM_DIAG_NO_HO 0   // fused tick: no hand-offs (TD reads the ring slot as written so far)
-#endif
-#ifndef SWARM_DIAG_ACT
-#define SWARM_DIAG_ACT 0     // fused tick: 1 = odd acting waves, 2 = every acting wave stops after Adam
-#endif
-
 namespace swarm {
 
 // ---------------------------------------------------------------- constants
@@ -175,18 +167,12 @@ __host__ __device__ inline uint32_t sample_position(uint32_t g, const SampleKey&
 // slab; the reduce launch sums column block j (16 columns) over all slabs in block order.
 // Layout: column-block major, [kSlabColBlocks][n_slabs][16], so one reduce block reads one
 // contiguous n_slabs x 64 B run (whole 128-B lines, each fetched by one block) instead of a
-// 64-B piece of every 6.7-KB slab row.  SWARM_SLAB_T = 0: the row-major [n_slabs][N_PARAMS + 1].
-#ifndef SWARM_SLAB_T
-#define SWARM_SLAB_T 1
-#endif
+// 64-B piece of every 6.7-KB slab row.
 constexpr int kSlabCols = 16;
 constexpr int kSlabColBlocks = (N_PARAMS + 1 + kSlabCols - 1) / kSlabCols;
-__host__ __device__ constexpr size_t slab_floats_per_block() {
-  return SWARM_SLAB_T ? (size_t)kSlabColBlocks * kSlabCols : (size_t)(N_PARAMS + 1);
-}
+__host__ __device__ constexpr size_t slab_floats_per_block() { return (size_t)kSlabColBlocks * kSlabCols; }
 __host__ __device__ inline size_t slab_index(int q, int b, int n_slabs) {
-  return SWARM_SLAB_T ? ((size_t)(q / kSlabCols) * n_slabs + b) * kSlabCols + (q % kSlabCols)
-                      : (size_t)b * (N_PARAMS + 1) + q;
+  return ((size_t)(q / kSlabCols) * n_slabs + b) * kSlabCols + (q % kSlabCols);
 }
 
 // ---------------------------------------------------------------- fused-tick hand-off
@@ -208,18 +194,6 @@ __device__ inline unsigned long long ld_granule(const unsigned long long* g) {
   return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one-launch tick (swarm_red.h): counters in the tick workspace, 64-bit words
-// {epoch << 16 | count}.  The epoch advances once per one-launch tick (its control role), so a
-// count never carries over from an earlier launch whatever happens to ctrl in between: an
-// incrementer raises the word to its epoch's base (atomicMax) before adding one.
-constexpr int kWsEpoch = 16, kWsActPro = 32, kWsTdDone = 48;   // u64 word indices, one 128-B line each
-__device__ inline unsigned long long red_epoch_load(const unsigned long long* ws) {
-  return __hip_atomic_load(ws + kWsEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void red_count(unsigned long long* w, unsigned long long epoch) {
-  __hip_atomic_fetch_max(w, epoch << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // ---------------------------------------------------------------- small math
 __host__ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * kLeakySlope; }
 

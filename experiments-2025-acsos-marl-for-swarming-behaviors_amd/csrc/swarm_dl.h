@@ -147,14 +147,9 @@ __device__ inline uint32_t knn_mask_node(int n, int N, int k, const WSmall<NS>& 
   return topk_smallest_mask<GS>(d, N, k, q);
 }
 
-// t-th (1-based) lowest / highest set bit of a lane mask
-__device__ inline int bit_sel_low(uint32_t m, int t) {
-  for (int i = 1; i < t; ++i) m &= m - 1u;
-  return __ffs(m) - 1;
-}
-__device__ inline int bit_sel_high(uint32_t m, int t) {
-  for (int i = 1; i < t; ++i) m &= ~(1u << (31 - __clz(m)));
-  return 31 - __clz(m);
+static __device__ inline void kv_heap_select_swap(KV* a, int first, int nth, int last) {
+  kv_heap_select(a, first, nth + 1, last);
+  kv_swap(a, first, nth);
 }
 
 // The boundary-tie rows of knn_masks_wave, G lanes per row (one element per lane, G >= the
@@ -169,123 +164,9 @@ __device__ inline int bit_sel_high(uint32_t m, int t) {
 // torch.topk on 60,000 tie-heavy rows (n 4..16) before it went in; the GPU tests compare the
 // sets with torch.topk (oracle knn_sets) and the recorded reference actions.
 // tb: ballot with bit n * lpn set for every tie row n; q: GS KV entries of LDS per slot.
-// A/B knobs: SWARM_TIE_NOINLINE = 1 keeps the (rarely taken) tie path out of line, so its
-// registers and code do not weigh on the caller; SWARM_DIAG_NO_TIE = 1 skips it (timing only:
-// wrong neighbour sets on tied rows, never shipped)
-#ifndef SWARM_TIE_NOINLINE
-#define SWARM_TIE_NOINLINE 0
-#endif
-#ifndef SWARM_DIAG_NO_TIE
-#define SWARM_DIAG_NO_TIE 0
-#endif
-#ifndef SWARM_TIE_LEGACY
-#define SWARM_TIE_LEGACY 0   // A/B: the round-3 branchy restatement (knn_tie_rows_wave_legacy)
-#endif
-#ifndef SWARM_TIE_MEMO
-#define SWARM_TIE_MEMO 1   // acting waves keep each slot's last tie result keyed by its rank signature
-#endif
-#ifndef SWARM_DIAG_TIE_COUNT
-#define SWARM_DIAG_TIE_COUNT 0   // diagnostic builds: count tie-path entries (rows) and calls (waves)
-#endif
-#if SWARM_DIAG_TIE_COUNT
-__device__ unsigned long long g_swarm_tie_rows, g_swarm_tie_calls, g_swarm_knn_calls;
-__device__ unsigned int g_swarm_tie_env[4096];   // tie builds per acting wave (block * 4 + wave)
-#endif
-static __device__ inline void kv_heap_select_swap(KV* a, int first, int nth, int last) {
-  kv_heap_select(a, first, nth + 1, last);
-  kv_swap(a, first, nth);
-}
-#if SWARM_TIE_NOINLINE
-#define SWARM_TIE_INLINE __attribute__((noinline))
-#else
-#define SWARM_TIE_INLINE inline
-#endif
-template <int NS, int GS>
-__device__ SWARM_TIE_INLINE void knn_tie_rows_wave_legacy(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
-                                                   const float* __restrict__ dn, KV* q) {
-  constexpr int G = GS <= 8 ? 8 : 16;   // lanes per row
-  constexpr int NG = 64 / G;
-  const int g = lane / G, e = lane % G, gb = lane - e;
-  auto gballot = [&](bool x) -> uint32_t { return (uint32_t)((__ballot(x) >> gb) & ((1ull << G) - 1ull)); };
-  while (tb) {
-    unsigned long long t = tb;
-    for (int i = 0; i < g && t; ++i) t &= t - 1ull;   // this group's row: the g-th remaining
-    for (int i = 0; i < NG && tb; ++i) tb &= tb - 1ull;
-    if (t == 0ull) continue;
-    const int n = (__ffsll((long long)t) - 1) / lpn;
-    float v = e < N ? dn[n * GS + e] : 0.0f;
-    int id = e;
-    const int nth = k - 1;
-    int first = 0, last = N;
-    int depth = 2 * floor_log2(N);
-    bool heap = false;
-    while (last - first > 3) {   // group-uniform control flow
-      if (depth == 0) { heap = true; break; }
-      --depth;
-      const int mid = first + (last - first) / 2;
-      const float vx = __shfl(v, gb + first + 1), vy = __shfl(v, gb + mid), vz = __shfl(v, gb + last - 1);
-      int pick;   // kv_move_median_to_first(first, first + 1, mid, last - 1)
-      if (vx < vy) pick = (vy < vz) ? mid : ((vx < vz) ? last - 1 : first + 1);
-      else if (vx < vz) pick = first + 1;
-      else pick = (vy < vz) ? last - 1 : mid;
-      int src = e == first ? pick : (e == pick ? first : e);
-      v = __shfl(v, gb + src);
-      id = __shfl(id, gb + src);
-      const float pv = __shfl(v, gb + first);
-      const uint32_t lm = gballot(e > first && e < last && !(v < pv));
-      const uint32_t rm = gballot(e >= first && e < last && !(pv < v));
-      const bool is_l = (lm >> e) & 1u, is_r = (rm >> e) & 1u;
-      const int tl = __popc(lm & ((1u << e) - 1u)) + 1;   // rank among the left stoppers
-      const int above = __popc(rm >> (e + 1));             // right stoppers after e
-      const int T = __popc(gballot(is_l && above >= tl));
-      src = e;
-      if (is_l && tl <= T) src = bit_sel_high(rm, tl);
-      if (is_r && above + 1 <= T) src = bit_sel_low(lm, above + 1);
-      v = __shfl(v, gb + src);
-      id = __shfl(id, gb + src);
-      int cut = __ffs(lm) - 1;
-      if (T > 0) {
-        cut = bit_sel_high(rm, T);
-        if (__popc(lm) > T) cut = min(cut, bit_sel_low(lm, T + 1));
-      }
-      if (cut <= nth) first = cut;
-      else last = cut;
-    }
-    if (heap) {   // depth limit: heap_select + swap, serially (kv_nth_element)
-      KV* a = q + n * GS;
-      if (e < N) a[e] = KV{v, id};
-      wave_lds_sync();
-      if (e == 0) kv_heap_select_swap(a, first, nth, last);
-      wave_lds_sync();
-      if (e < N) { v = a[e].v; id = a[e].i; }
-    } else {      // kv_insertion_sort of [first, last), <= 3 elements: stable rank sort
-      const bool in = e >= first && e < last;
-      int rank = 0;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int pj = first + j;
-        const float vj = __shfl(v, gb + min(pj, G - 1));
-        if (pj < last) rank += (vj < v || (vj == v && pj < e)) ? 1 : 0;
-      }
-      const uint32_t r0 = gballot(in && rank == 0), r1 = gballot(in && rank == 1), r2 = gballot(in && rank == 2);
-      const uint32_t rm = e - first == 0 ? r0 : (e - first == 1 ? r1 : r2);
-      const int src = in ? __ffs(rm) - 1 : e;
-      v = __shfl(v, gb + src);
-      id = __shfl(id, gb + src);
-    }
-    uint32_t mm = e < k ? (1u << id) : 0u;
-#pragma unroll
-    for (int s = G / 2; s >= 1; s >>= 1) mm |= (uint32_t)__shfl_xor((int)mm, s);
-    if (e == 0) sm.knn[n] = mm;
-  }
-}
-
-
-// The boundary-tie rows, straight-line: the same restatement as knn_tie_rows_wave_legacy
-// (libstdc++ introselect on G lanes per row: median-of-3 swap, one-step unguarded partition,
-// rank-sort finish, serial heap_select at the depth limit) with every per-group decision a
-// select instead of a branch.  Rows whose count test fails in a formation that persists
-// (stacked agents keep a boundary tie every tick) run this every tick at one wave per SIMD,
+// Every per-group decision is a select instead of a branch.  Rows whose count test fails in a
+// formation that persists (stacked agents keep a boundary tie every tick) run this every tick
+// at one wave per SIMD,
 // where a wave issues one instruction per 4 cycles: its instruction count is the acting
 // launch's tail, hence the shape of a round:
 //  - one hop of four values (the one at `first` and the three median candidates); the median
@@ -300,8 +181,8 @@ __device__ SWARM_TIE_INLINE void knn_tie_rows_wave_legacy(int lane, int N, int k
 // left of `first` plus the range's elements whose stable rank (kv_insertion_sort's order) is
 // at most nth - first.  q: the wave's KV scratch, reused as the L / R rows (2 G ints per group).
 template <int NS, int GS>
-__device__ SWARM_TIE_INLINE void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
-                                                   const float* __restrict__ dn, KV* q) {
+__device__ inline void knn_tie_rows_wave(int lane, int N, int k, unsigned long long tb, int lpn, WSmall<NS>& sm,
+                                         const float* __restrict__ dn, KV* q) {
   constexpr int G = GS <= 8 ? 8 : 16;   // lanes per row
   constexpr int NG = 64 / G;
   static_assert(NG * 2 * G <= 2 * NS * GS, "L / R rows fit the KV scratch");
@@ -461,7 +342,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
   const bool tie = r == 0 && nvalid && __popc(mask) != k;
   bool hit = false;
   uint32_t hit_mask = 0u;
-  if (SWARM_TIE_MEMO && memo) {
+  if (memo) {
     // OR the slot's LPN lanes (aligned groups inside a 16-lane row): quad xor 1, quad xor 2,
     // and for 8-lane slots the half-row mirror
     sig_lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sig_lo, 0xB1, 0xF, 0xF, false);
@@ -483,26 +364,15 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
   if (r == 0) sm.knn[n] = nvalid ? (hit ? hit_mask : mask) : 0u;
   const bool run = tie && !hit;
   const unsigned long long tb = __ballot(run);
-#if SWARM_DIAG_TIE_COUNT
-  if (lane == 0) {
-    atomicAdd(&g_swarm_knn_calls, 1ull);
-    if (tb) {
-      atomicAdd(&g_swarm_tie_calls, 1ull);
-      atomicAdd(&g_swarm_tie_rows, (unsigned long long)__popcll(tb));
-      atomicAdd(&g_swarm_tie_env[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 4095], 1u);
-    }
-  }
-#endif
-  if (!SWARM_DIAG_NO_TIE && tb != 0ull) {
+  if (tb != 0ull) {
     // boundary ties: the introselect restatement, G lanes per row
 #if SWARM_STAMPS   // stamps build: per-wave tie-path entries (slot 27) and s_memtime cycles in it (slot 28)
     const long long s0 = clock64();
 #endif
     wave_lds_sync();
-    if (SWARM_TIE_LEGACY) knn_tie_rows_wave_legacy<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
-    else knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
+    knn_tie_rows_wave<NS, GS>(lane, N, k, tb, LPN, sm, dn, q);
     wave_lds_sync();
-    if (SWARM_TIE_MEMO && memo && run) {
+    if (memo && run) {
       memo->sig_lo[n] = sig_lo;
       memo->sig_hi[n] = sig_hi;
       memo->mask[n] = sm.knn[n];
@@ -519,7 +389,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
 #endif
   }
 #if SWARM_STAMPS
-  if (SWARM_TIE_MEMO && memo && g_swarm_stamps && lane == 0 && __ballot(hit) != 0ull)   // slot 18: memo hits
+  if (memo && g_swarm_stamps && lane == 0 && __ballot(hit) != 0ull)   // slot 18: memo hits
     g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + 18] += 1ull;
 #endif
 }

@@ -8,7 +8,6 @@
 
 #include "swarm_tdk.h"
 #include "swarm_peer.h"
-#include "swarm_red.h"
 
 namespace swarm {
 
@@ -47,17 +46,72 @@ struct ReduceArgs {
 // reproducible run to run.  Advance mode adds one control block (the last): it prepares
 // and stores the whole ctrl update (Adam scalars of the next step in double, the next
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
-// kRedCols = 16 columns x kRedGroups = 64 slab groups per block (swarm_red.h, shared with the
-// one-launch tick's column roles, which must sum in this exact order)
-#ifndef SWARM_RED_COPY_BLOCKS
-#define SWARM_RED_COPY_BLOCKS 1
-#endif
-constexpr int kRedCopyBlocks = SWARM_RED_COPY_BLOCKS ? 3 : 0;
-// A/B knob: 1 = the 64 group sums of a column combined by permlane swaps within each wave, then
-// the 16 wave sums (one barrier); 0 = two LDS levels (8 runs of 8, then the runs; two barriers)
-#ifndef SWARM_RED_DPP
-#define SWARM_RED_DPP 0
-#endif
+// Three more blocks copy w / m / v _nxt -> _cur (one array each), beside the column blocks.
+constexpr int kRedCols = 16;      // columns per reduce block
+constexpr int kRedGroups = 64;    // slab groups per column (consecutive slabs each)
+constexpr int kRedRuns = kRedGroups / 8;
+constexpr int kRedChunk = 8;      // slabs per load chunk of a group
+constexpr int kRedColBlocks = (N_PARAMS + 1 + kRedCols - 1) / kRedCols;
+constexpr int kRedCopyBlocks = 3;
+
+// ---- the ctrl advance of one tick (the reduce launch's control block).  Every thread of the
+//      block calls it; thread 0 advances the counters and the Adam scalars, thread 64 derives the
+//      next tick's sampling key; both read ctrl before the barrier and write after it.
+struct RedCtrl {
+  int capacity, B, batch;
+  swarm_adam_cfg hp;
+  uint32_t k0, k1;   // replay-sampling key (seed ^ rank salt)
+};
+
+__device__ inline void red_control(swarm_ctrl* C, const RedCtrl& A) {
+  const int t = threadIdx.x;
+  uint32_t c_trained = 0, c_step = 0, c_tick = 0, c_slot = 0, c_filled = 0;
+  double b1p = 1.0, b2p = 1.0;
+  float next_step_size = 0.0f, next_inv_bc2 = 0.0f;
+  SampleKey nk = {};
+  uint32_t nk_n = 0, nk_tick = 0;
+  const uint32_t cap = (uint32_t)A.capacity;
+  if (t == 0) {
+    // a held rank (peer_hold: an expired exchange wait) applied no step this tick
+    c_trained = C->peer_hold ? 0u : C->trained;
+    c_step = C->adam_step; c_tick = C->tick; c_slot = C->write_slot; c_filled = C->filled_slots;
+    b1p = ctrl_get_double(C, CTRL_B1POW);
+    b2p = ctrl_get_double(C, CTRL_B2POW);
+    if (c_trained) {   // the step this tick's act kernel applied
+      b1p = b1p * (double)A.hp.beta1;
+      b2p = b2p * (double)A.hp.beta2;
+      adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
+    }
+  } else if (t == 64) {
+    const uint32_t filled = C->filled_slots;
+    const uint32_t f1 = filled + 1 < cap ? filled + 1 : cap;   // filled after this tick
+    nk_n = (f1 + 1 < cap ? f1 + 1 : cap) * (uint32_t)A.B;       // graphs the next tick samples from
+    nk_tick = C->tick + 1;
+    nk = sample_key(nk_n, A.k0, A.k1, nk_tick);
+  }
+  __syncthreads();
+  if (t == 0) {   // record the pending update, advance the tick
+    const uint32_t valid_slots = c_filled + 1 < cap ? c_filled + 1 : cap;
+    const uint32_t trained = valid_slots * (uint32_t)A.B >= (uint32_t)A.batch ? 1u : 0u;
+    if (c_trained) {
+      C->adam_step = c_step + 1;
+      ctrl_set_double(C, CTRL_B1POW, b1p);
+      ctrl_set_double(C, CTRL_B2POW, b2p);
+      C->adam_step_size = next_step_size;
+      C->adam_inv_bc2 = next_inv_bc2;
+    }
+    C->trained = trained;
+    C->tick = c_tick + 1;
+    C->write_slot = (c_slot + 1) % cap;
+    C->filled_slots = valid_slots;
+  } else if (t == 64) {
+    C->sample_key[0] = nk.rk[0]; C->sample_key[1] = nk.rk[1]; C->sample_key[2] = nk.rk[2]; C->sample_key[3] = nk.rk[3];
+    C->sample_bits = (uint32_t)nk.bits;
+    C->sample_n = nk_n;
+    C->sample_tick = nk_tick;
+  }
+}
+
 static_assert(kRedGroups % 8 == 0 && kRedCols * kRedGroups <= 1024, "reduce geometry");
 static_assert(kRedColBlocks <= kPeerSeqRegion, "peer seq region");
 // slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start.
@@ -73,14 +127,14 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
   swarm_ctrl* C = ctrl;
-  if (kRedCopyBlocks && (int)blockIdx.x > kRedColBlocks) {   // advance mode: a copy-back block
+  if ((int)blockIdx.x > kRedColBlocks) {   // advance mode: a copy-back block
     const int j = (int)blockIdx.x - kRedColBlocks - 1;
     const float4* src = reinterpret_cast<const float4*>(j == 0 ? A.lr.w_nxt : (j == 1 ? A.lr.m_nxt : A.lr.v_nxt));
     float4* dst = reinterpret_cast<float4*>(j == 0 ? A.lr.w_cur : (j == 1 ? A.lr.m_cur : A.lr.v_cur));
     if ((int)threadIdx.x < N_PARAMS_PAD / 4) dst[threadIdx.x] = src[threadIdx.x];
     return;
   }
-  if ((int)blockIdx.x == kRedColBlocks) {   // advance mode: the control block (swarm_red.h)
+  if ((int)blockIdx.x == kRedColBlocks) {   // advance mode: the control block (red_control)
     RedCtrl rc;
     rc.capacity = A.capacity; rc.B = A.B; rc.batch = A.batch; rc.hp = A.hp; rc.k0 = A.k0; rc.k1 = A.k1;
     red_control(C, rc);
@@ -109,27 +163,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
       for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }
   }
-  if (!kRedCopyBlocks && advance && col < N_PARAMS) {   // ping-pong copy-back, one array per group
-    if (q == 0) A.lr.w_cur[col] = A.lr.w_nxt[col];
-    else if (q == 1) A.lr.m_cur[col] = A.lr.m_nxt[col];
-    else if (q == 2) A.lr.v_cur[col] = A.lr.v_nxt[col];
-  }
   SWARM_STAMP(29);
-#if SWARM_RED_DPP
-  // the four groups of a wave (lanes c, c + 16, c + 32, c + 48) combined by permlane swaps, then
-  // the kRedGroups / 4 wave sums of a column in wave order: one block barrier
-  static_assert(kRedCols == 16, "one column per lane of a 16-lane row");
-  {
-    const float ws = row4_sum(s);
-    if ((threadIdx.x & 63) < kRedCols) part[threadIdx.x >> 6][c] = ws;
-  }
-  __syncthreads();
-  SWARM_STAMP(30);
-  if (q == 0 && col <= N_PARAMS) {
-    float tot = part[0][c];
-#pragma unroll
-    for (int gi = 1; gi < kRedGroups / 4; ++gi) tot = tot + part[gi][c];
-#else
   part[q][c] = s;
   __syncthreads();
   SWARM_STAMP(30);
@@ -144,7 +178,6 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     float tot = part2[0][c];
 #pragma unroll
     for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
-#endif
     if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
     else A.grad[col] = tot;
     // this rank's loss of the update (0 when skipped: the TD launch wrote zero slabs)

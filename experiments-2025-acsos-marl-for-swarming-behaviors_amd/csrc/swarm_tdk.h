@@ -74,16 +74,8 @@ struct TdArgs {
 };
 
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
-// measured against nt (1: td 8.4 vs 8.0 us) and write-through sc1 (2: 9.5 us) stores.
-__device__ inline void slab_st(float* p, float v) {
-#if SWARM_SLAB_ST == 1
-  __builtin_nontemporal_store(v, p);
-#elif SWARM_SLAB_ST == 2
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (sc1)
-#else
-  *p = v;
-#endif
-}
+// measured against nt (td 8.4 vs 8.0 us) and write-through sc1 (9.5 us) stores.
+__device__ inline void slab_st(float* p, float v) { *p = v; }
 
 // D[i][j] = sum_node A_img[node][i] * B_img[node][j] over the 32 node rows (MFMA, K = node)
 // (all 32 operands read first: no LDS round trip between two steps of the MFMA chain)
@@ -120,7 +112,6 @@ struct TdFused {
   swarm_adam_cfg hp;
   const unsigned long long* ho_rec;   // [B][ho_stride_granules(N)] tagged hand-off records
   uint32_t* ho_err;                   // bounded-wait overruns (0 in a correct run)
-  unsigned long long* red_ws;         // one-launch tick (swarm_red.h): the workspace's counter words
 };
 #ifndef SWARM_HO_SPIN_LIMIT
 #define SWARM_HO_SPIN_LIMIT (1 << 18)
@@ -168,15 +159,7 @@ __device__ inline void drop_overrun(const bool (&okc)[DGeom<NS>::CT], bool (&dro
     if (bad[ct]) { drop[ct] = true; nv[ct] = false; }
 }
 
-// a TD block's slab granules are issued -> count it (no drain: the granules carry their own tags)
-__device__ inline void red_td_done_cnt(unsigned long long* ws, unsigned long long epoch) {
-  __syncthreads();
-  if (threadIdx.x == 0) red_count(ws + kWsTdDone, epoch);
-}
-
-// RED (fused only): the one-launch tick (swarm_red.h): the slab goes out as tagged granules and
-// the block counts itself done, for the acting blocks' reduce roles
-template <int NS, int GS, int SPEC, bool FUSED = false, bool RED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
+template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
                                         const float* rs_next, const float* rr, const uint8_t* ra, int S, int B,
                                         int N, int capacity, const TdArgs& A, const TdFused& X,
@@ -187,6 +170,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   constexpr int GPW = NS / GS;                             // graphs per wave
   constexpr int NT = 128 * GPB;
   static_assert(!FUSED || NT == kAdamNT, "the fused TD block is one Adam workgroup");
+  static_assert(GPB <= 2, "B2 jobs 2 and 3 go to the pre-path online waves by wave index (GPB <= 2)");
   TdLds<NS>& TB = L.TB;
   float* Pon = L.Pon;
   float* Ptg = L.Ptg;
@@ -199,16 +183,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.target_view(wi);
   const int lane = d.lane, c = d.c, p = d.p;
-  // this block's slab column q (swarm_common.h slab_index: column-block major); RED: granules
-  static_assert(!RED || FUSED, "the one-launch tick is a fused tick");
-  uint32_t red_tag = 0u;   // RED: this tick's tag (tick + 1), set once ctrl is read
-  auto sst = [&](int q, float v) {
-    if constexpr (RED) {
-      st_granule(reinterpret_cast<unsigned long long*>(A.slabs) + slab_index(q, vb, A.n_slabs), red_tag, __float_as_uint(v));
-    } else {
-      slab_st(A.slabs + slab_index(q, vb, A.n_slabs), v);
-    }
-  };
+  // this block's slab column q (swarm_common.h slab_index: column-block major)
+  auto sst = [&](int q, float v) { slab_st(A.slabs + slab_index(q, vb, A.n_slabs), v); };
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
@@ -228,11 +204,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // write_slot, the batch size S, the Adam hyper-parameters) made opaque here, so they are
   // loaded with the first scalar wait instead of being re-fetched at a later first use behind a
   // second one (a kernarg / ctrl round trip on the TD chain)
-  unsigned long long red_epoch = 0ull;
-  if constexpr (RED) {
-    red_tag = cc.tick + 1u;
-    red_epoch = red_epoch_load(X.red_ws);
-  }
   swarm_adam_cfg hp = X.hp;
   int32_t* sample_out = A.sample_out;
   const unsigned long long* ho_rec = X.ho_rec;
@@ -280,7 +251,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const bool cur = live[ct] && n_graphs >= (uint32_t)S && gid[ct] / (uint32_t)B == wslot;
-    ho[ct] = FUSED && !SWARM_DIAG_NO_HO && cur;
+    ho[ct] = FUSED && cur;
     wait = wait || ho[ct];
     inslot = inslot || cur;
   }
@@ -304,7 +275,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
   if (n_graphs < (uint32_t)S) {
     for (int q = threadIdx.x; q <= N_PARAMS; q += NT) sst(q, 0.0f);
-    if constexpr (RED) red_td_done_cnt(X.red_ws, red_epoch);
     return;
   }
   if (sample_out && online && p == 0) {
@@ -862,7 +832,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   SWARM_STAMP(7);
   SWARM_RTSTAMP(9);
-  if constexpr (RED) red_td_done_cnt(X.red_ws, red_epoch);
 }
 
 }  // namespace swarm

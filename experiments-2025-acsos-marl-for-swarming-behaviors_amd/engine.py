@@ -10,12 +10,6 @@ One fused training tick (the reference's hot loop, src/training/train_gcn_dqn.py
     swarm_reduce_advance  deterministic slab sum, ping-pong copy-back, ctrl advance    (1 launch)
     [all_reduce(grad) over RCCL when world_size > 1]
 
-Opt-in (SWARM_TICK_REDUCE=1; one rank, n_agents <= 8, >= 425 envs): the reduce launch folds
-into the tick launch (``tick_reduce``, SWARM_F_TICK_REDUCE, csrc/swarm_red.h): the acting
-blocks, once their env is stepped, sum the TD blocks' tagged slab granules in the reduce
-launch's exact order, copy the learner rows back and advance ctrl.  Bit-identical, but slower
-on MI355X, so the two-launch tick stays the default.
-
 With a ``PeerExchange`` (dist.py; ``peer=``) the all-reduce is fused into the reduce launch
 (``swarm_reduce_advance_peer``: xGMI stores of the column sums, rank-ordered sum): still two
 launches per tick at any world size, and no collective in the captured graph.
@@ -37,8 +31,6 @@ Every launch goes to torch's current stream, so a run of ticks can be captured
 once into a hipGraph (``capture``) and replayed.  There is no CPU fallback.
 """
 from __future__ import annotations
-
-import os
 
 import math
 from typing import Optional
@@ -185,20 +177,7 @@ class SwarmEngine:
         if ws < 0:
             check(int(ws), "swarm_td_workspace_floats")
         self.fused = learn and bool(self.lib.swarm_train_tick_supported(ctypes_ref(self.cfg)))
-        # one launch per tick (SWARM_F_TICK_REDUCE, swarm_red.h): the slab reduce and the ctrl
-        # advance inside the tick kernel.  Measured slower (30.7 vs 14.4 us per tick at C2,
-        # profiles/r03_ab_tick_reduce.jsonl: the cross-XCD polling and the write-through slab
-        # granules cost more than the launch boundary they remove), so opt-in only:
-        # SWARM_TICK_REDUCE=1.  One rank only (world_size > 1 exchanges in the reduce launch)
-        self.tick_reduce = (self.fused and world_size == 1 and peer is None
-                            and os.environ.get("SWARM_TICK_REDUCE", "0") == "1"
-                            and bool(self.lib.swarm_train_tick_reduce_supported(ctypes_ref(self.cfg),
-                                                                                ctypes_ref(self.hp))))
-        self.cfg_tick = SwarmConfig.from_buffer_copy(self.cfg)
-        if self.tick_reduce:
-            self.cfg_tick.flags |= _lib.F_TICK_REDUCE
-        # the one-launch tick stores its slabs as tagged 8-byte granules
-        self.slabs = torch.zeros(int(ws) * (2 if self.fused else 1), **f32)
+        self.slabs = torch.zeros(int(ws), **f32)
         self.grad = torch.zeros(N_PARAMS + 3, **f32)
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
@@ -330,8 +309,8 @@ class SwarmEngine:
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
     def launch_tick(self, full_out: bool = False):
-        """The fused tick's launch; with tick_reduce it also reduces and advances ctrl."""
-        check(self.lib.swarm_train_tick(ctypes_ref(self.cfg_tick), ctypes_ref(self.hp), ctypes_ref(self.learner),
+        """The fused tick's launch (acting + TD blocks); swarm_reduce_advance follows it."""
+        check(self.lib.swarm_train_tick(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
                                         ptr(self.state), ctypes_ref(self.replay), ptr(self.ctrl),
                                         ctypes_ref(self.out if full_out else self.out_min), ptr(self.slabs),
                                         ptr(self.tick_ws), ptr(self.samples), stream_ptr()), "swarm_train_tick")
@@ -372,8 +351,6 @@ class SwarmEngine:
         if not self.fused:
             return self.train_tick3(full_out)
         self.launch_tick(full_out)
-        if self.tick_reduce:
-            return
         self.launch_reduce_advance()
         if self.peer is None:
             self.allreduce_grad()

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 8
+#define SWARM_ABI_VERSION 9
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
@@ -63,7 +63,6 @@ typedef struct swarm_config {
 
 #define SWARM_F_SHARED_RESET 1   /* one reset centre for all envs (go_to_position_scenario.py:88) */
 #define SWARM_F_RANDOM_OA 2      /* ObstacleAvoidance random=True (obstacle_avoidance_scenario.py:100) */
-#define SWARM_F_TICK_REDUCE 4    /* swarm_train_tick: the slab reduce + ctrl advance in the same launch */
 
 /* Device-resident control block; kernels read and advance it so that a tick
  * sequence can be replayed from a captured hipGraph.  Layout is ABI. */
@@ -219,17 +218,6 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
  * Complete, kNN or radius training graph, GAT or GCNConv, n_agents <= 16; else SWARM_E_UNSUPPORTED. */
 int swarm_train_tick_supported(const swarm_config* cfg);
 int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg);
-/* cfg->flags & SWARM_F_TICK_REDUCE: ONE launch per tick.  The acting blocks, once their env is
- * stepped, also do swarm_reduce_advance's work (slab sum in its exact order, copy-back, ctrl
- * advance); the TD blocks store their slab as tagged granules, so `slabs` must hold
- * 2 x swarm_td_workspace_floats floats.  Do not follow with swarm_reduce_advance.  Needs
- * world_size 1, n_agents <= 8, n_envs >= 425 (107 acting blocks) and a TD batch of <= 512 blocks:
- * swarm_train_tick_reduce_supported; else SWARM_E_UNSUPPORTED.  Bit-identical to the two-launch
- * tick, but slower on MI355X (30.7 vs 14.4 us per tick at C2: cross-XCD polling and write-through
- * granules cost more than the launch boundary they remove), so the engine only uses it when asked
- * (SWARM_TICK_REDUCE=1).  Replaces nothing in the reference: its tick is a Python loop
- * (train_gcn_dqn.py:153-178). */
-int swarm_train_tick_reduce_supported(const swarm_config* cfg, const swarm_adam_cfg* hp);
 int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
                      const swarm_replay* replay, const swarm_ctrl* ctrl, const swarm_act_out* out,
                      float* slabs, void* workspace, int32_t* sample_out, void* stream);

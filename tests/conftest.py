@@ -10,21 +10,36 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 # achieved errors of every numeric comparison, written at session end (record the
-# observed margins, not just pass/fail).  The GPU runs copy it to profiles/.
-ERRORS_OUT = os.environ.get("SWARM_PARITY_ERRORS", os.path.join(ROOT, "gpurun_out", "parity_errors.json"))
+# observed margins, not just pass/fail) to gpurun_out/parity_errors.<kind>.json, kind = "gpu" when
+# the session ran a test marked gpu, else "cpu": a CPU run never overwrites a GPU run's margins.
+# The GPU runs copy the gpu file to profiles/.
+ERRORS_DIR = os.path.join(ROOT, "gpurun_out")
 _RECORDS = []
+_RAN_GPU = []
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built libswarm_hip.so")
 
 
+def pytest_runtest_setup(item):
+    if item.get_closest_marker("gpu") is not None:
+        _RAN_GPU.append(item.nodeid)
+
+
+def errors_path(ran_gpu: bool) -> str:
+    return os.environ.get("SWARM_PARITY_ERRORS") or os.path.join(
+        ERRORS_DIR, "parity_errors.%s.json" % ("gpu" if ran_gpu else "cpu"))
+
+
 def pytest_sessionfinish(session, exitstatus):
     if not _RECORDS:
         return
-    os.makedirs(os.path.dirname(ERRORS_OUT), exist_ok=True)
-    with open(ERRORS_OUT, "w") as f:
-        json.dump({"exitstatus": int(exitstatus), "records": _RECORDS}, f, indent=0)
+    out = errors_path(bool(_RAN_GPU))
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump({"exitstatus": int(exitstatus), "kind": "gpu" if _RAN_GPU else "cpu", "records": _RECORDS}, f,
+                  indent=0)
 
 
 @pytest.fixture(scope="session")

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     for n in sorted(names):
         assert hasattr(raw, n), n
     assert names == set(L.EXPORTED)
-    assert lib.swarm_abi_version() == L.ABI_VERSION == 8 and lib.swarm_n_params() == O.N_PARAMS
+    assert lib.swarm_abi_version() == L.ABI_VERSION == 9 and lib.swarm_n_params() == O.N_PARAMS
 
 
 def test_topk_emulation_matches_torch_fixture():
@@ -198,15 +198,6 @@ def test_fused_tick_support_and_workspace_host_side():
     lr = L.SwarmLearner(*([1] * 8))
     rp = L.SwarmReplay(1, 1, 1, 1, 4, 0)
     args = (ctypes.byref(hp), ctypes.byref(lr), 1, ctypes.byref(rp), 1, None, 1, 1, None, None)
-    # the opt-in one-launch tick (SWARM_F_TICK_REDUCE): one rank, <= 8 agents, >= 107 acting
-    # blocks, <= 512 TD blocks
-    assert lib.swarm_train_tick_reduce_supported(ctypes.byref(ok[0]), ctypes.byref(hp)) == 1
-    assert lib.swarm_train_tick_reduce_supported(ctypes.byref(cfg(N=12)), ctypes.byref(hp)) == 0
-    assert lib.swarm_train_tick_reduce_supported(ctypes.byref(cfg(B=256)), ctypes.byref(hp)) == 0
-    hp2 = L.SwarmAdamCfg(1e-3, 0.9, 0.999, 1e-8, 1.0, 0.99, 32, 200, 2, 0)
-    assert lib.swarm_train_tick_reduce_supported(ctypes.byref(ok[0]), ctypes.byref(hp2)) == 0
-    hp4k = L.SwarmAdamCfg(1e-3, 0.9, 0.999, 1e-8, 1.0, 0.99, 4096, 200, 1, 0)
-    assert lib.swarm_train_tick_reduce_supported(ctypes.byref(ok[0]), ctypes.byref(hp4k)) == 0
     assert lib.swarm_train_tick(ctypes.byref(bad[0]), *args) == -4
     assert lib.swarm_train_tick(ctypes.byref(ok[0]), *args[:6], 1, None, None, None) == -1   # no workspace
     # the three-layer GAT (Flocking checkpoints) is forward only: every learner entry point refuses it

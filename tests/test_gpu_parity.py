@@ -646,64 +646,33 @@ def test_one_launch_tick_equals_three_launch_tick(sw, golden_weights, scen, N, c
     assert slots > 100 or n_cur > 0   # the hand-off path really ran
 
 
-@pytest.mark.parametrize("scen,N,conv,B,slots,graph", [("GoTo", 8, "gat", 512, 1, "complete"),
-                                                        ("GoTo", 8, "gat", 1024, 2, "complete"),
-                                                        ("GoTo", 8, "gcn", 512, 2, "knn"),
-                                                        ("ObstacleAvoidance", 5, "gat", 512, 2, "complete"),
-                                                        ("Flocking", 8, "gat", 640, 2, "complete"),
-                                                        ("GoTo", 6, "gat", 700, 3, "radius")])
-def test_single_launch_tick_reduce_equals_three_launch_tick(sw, golden_weights, monkeypatch, scen, N, conv, B, slots,
-                                                           graph):
-    """One launch per tick (SWARM_F_TICK_REDUCE, csrc/swarm_red.h): the acting blocks also do
-    the slab reduce (tagged granules, the reduce launch's exact summation order), the copy-back
-    and the ctrl advance.  Bit for bit the 3-launch tick, every tick, including a 3-launch tick
-    and a bare ctrl advance in the middle of the run (the in-kernel counters are epoch-stamped,
-    so nothing carries over between launches).  Opt-in mode (SWARM_TICK_REDUCE=1)."""
-    p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 2)
-    kw = dict(seed=9, params=p, batch=B, eps=0.3, update_target_every=3, replay_capacity=slots * B, conv=conv,
-              graph=graph, knn_k=5, radius=0.25)
-    monkeypatch.setenv("SWARM_TICK_REDUCE", "1")
-    a = sw.SwarmEngine(scen, N, B, **kw)
-    monkeypatch.setenv("SWARM_TICK_REDUCE", "0")
-    b = sw.SwarmEngine(scen, N, B, **kw)
-    assert a.tick_reduce
-    a.reset(0)
-    b.reset(0)
-    for t in range(12):
-        if t == 6:   # a 3-launch tick on a, then a bare advance on both
-            a.train_tick3(full_out=True)
-            b.train_tick3(full_out=True)
-            a.advance()
-            b.advance()
-        else:
-            a.train_tick(full_out=True)
-            b.train_tick3(full_out=True)
+@pytest.mark.parametrize("scen,N,graph", [("GoTo", 8, "complete"), ("ObstacleAvoidance", 5, "knn")])
+def test_seed_set_after_construction_reaches_the_fused_tick(sw, golden_weights, scen, N, graph):
+    """Environment.reset(seed=...) writes engine.cfg.seed after construction.  The
+    fused tick must draw with the new seed exactly as the 3-launch tick does (it once launched
+    with a copy of the config taken at construction)."""
+    p = _params(golden_weights, "go_to" if scen == "GoTo" else "obstacle_avoidance", 1)
+    kw = dict(seed=3, params=p, batch=256, eps=0.5, update_target_every=4, replay_capacity=2 * 256, graph=graph,
+              knn_k=3)
+    a, b, c = (sw.SwarmEngine(scen, N, 256, **kw) for _ in range(3))
+    assert a.fused
+    for e in (a, b, c):
+        e.reset(0)
+    diverged = False
+    for t in range(8):
+        if t == 3:
+            a.cfg.seed = 77
+            b.cfg.seed = 77
+        a.train_tick(full_out=True)
+        b.train_tick3(full_out=True)
+        c.train_tick(full_out=True)   # keeps seed 3
         torch.cuda.synchronize()
-        ca, cb = a.read_ctrl(), b.read_ctrl()
-        assert ca == cb, t
+        assert a.read_ctrl() == b.read_ctrl(), t
+        assert torch.equal(a.actions, b.actions) and torch.equal(a.samples, b.samples), t
         assert torch.equal(a.grad, b.grad), t
-        assert torch.equal(a.q, b.q) and torch.equal(a.actions, b.actions) and torch.equal(a.reward, b.reward), t
-        assert torch.equal(a.params, b.params) or t == 0, t
-    a.flush()
-    b.flush()
-    torch.cuda.synchronize()
-    assert torch.equal(a.params, b.params) and torch.equal(a.target, b.target)
-    assert torch.equal(a.adam_m, b.adam_m) and torch.equal(a.adam_v, b.adam_v)
-    assert torch.equal(a.state, b.state) and torch.equal(a.rep_s1, b.rep_s1) and torch.equal(a.rep_a, b.rep_a)
+        diverged = diverged or not torch.equal(a.actions, c.actions)
+    assert diverged   # the new seed took effect (eps 0.5: the coins and random actions changed)
     assert a.handoff_errors() == 0
-
-
-def test_single_launch_tick_reduce_gating(sw, golden_weights, monkeypatch):
-    """Which engines take the one-launch tick: opted in (SWARM_TICK_REDUCE=1), one rank,
-    n_agents <= 8, >= 107 acting blocks, a TD batch of <= 512 blocks."""
-    p = _params(golden_weights, "go_to", 1)
-    assert not sw.SwarmEngine("GoTo", 8, 512, seed=1, params=p).tick_reduce   # off by default
-    monkeypatch.setenv("SWARM_TICK_REDUCE", "1")
-    assert sw.SwarmEngine("GoTo", 8, 512, seed=1, params=p).tick_reduce
-    assert not sw.SwarmEngine("GoTo", 8, 256, seed=1, params=p).tick_reduce          # 64 acting blocks
-    assert not sw.SwarmEngine("GoTo", 12, 512, seed=1, params=p).tick_reduce         # 16-slot kernel
-    assert not sw.SwarmEngine("GoTo", 8, 4096, seed=1, params=p).tick_reduce         # 1024 TD blocks
-    assert not sw.SwarmEngine("GoTo", 8, 512, seed=1, params=p, world_size=2).tick_reduce
 
 
 def test_handoff_overrun_drops_the_waiting_graphs(sw, golden_weights):

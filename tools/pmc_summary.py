@@ -5,7 +5,11 @@ FETCH_SIZE / WRITE_SIZE are in KB per dispatch; on gfx950 FETCH_SIZE reports hal
 bytes of a wide coalesced read, so it is doubled (MI355X_MICROARCH.md §HBM).  Both count
 Infinity-Cache hits, so the figure is fabric traffic below L2, an upper bound on HBM.
 
-usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc_tick.json
+The summary records the library the passes profiled: the "build" object of the bench JSON line
+each pass printed (swarm_build_info() with its source digest, and the .so's sha256).  Every pass
+must name the same build; bench.py uses a summary's counters only for that build.
+
+usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r04_pmc_tick.json
 """
 import collections
 import csv
@@ -18,7 +22,25 @@ import sys
 KERNELS = {"tick": "tick_kernel", "td": "td_kernel", "act": "act_kernel<8, 1>", "reduce": "grad_reduce_kernel"}
 
 
+def pass_builds(src):
+    """The "build" object of the bench line in every pass log (p1.log, p2.log, ...)."""
+    builds = {}
+    for f in sorted(glob.glob(os.path.join(src, "p*.log"))):
+        for line in open(f, errors="replace"):
+            line = line.strip()
+            if line.startswith("{") and '"build"' in line:
+                try:
+                    builds[os.path.basename(f)] = json.loads(line)["build"]
+                except (ValueError, KeyError):
+                    pass
+    return builds
+
+
 def main(src, dst):
+    builds = pass_builds(src)
+    distinct = {json.dumps(b, sort_keys=True) for b in builds.values()}
+    if len(distinct) != 1:
+        raise SystemExit(f"pass logs name {len(distinct)} builds (need exactly one): {builds}")
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(src, "p*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
@@ -27,6 +49,7 @@ def main(src, dst):
                     vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
     out = {"source": "rocprofv3 --kernel-trace --pmc, separate passes (scripts/pmc.sh), bench.py workload",
            "units": "counter medians per dispatch; *_bytes in bytes",
+           "build": next(iter(builds.values())), "passes": sorted(builds),
            "kernels": {}}
     for key in KERNELS:
         k = {c: statistics.median(v) for (kk, c), v in vals.items() if kk == key}
