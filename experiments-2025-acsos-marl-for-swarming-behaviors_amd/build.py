@@ -50,8 +50,10 @@ def up_to_date() -> bool:
 STAMPS_OUT = os.path.join(HERE, "libswarm_hip_stamps.so")
 # test-only variant: every fused-tick hand-off wait overruns at once (tests of the drop path)
 HODROP_OUT = os.path.join(HERE, "libswarm_hip_hodrop.so")
+# diagnostic variant: in-kernel realtime launch stamps only (tools/tick_split_stamps.py)
+RTSTAMPS_OUT = os.path.join(HERE, "libswarm_hip_rtstamps.so")
 VARIANTS = {"main": (OUT, []), "stamps": (STAMPS_OUT, ["-DSWARM_STAMPS=1"]),
-            "hodrop": (HODROP_OUT, ["-DSWARM_HO_FORCE_DROP=1"])}
+            "rtstamps": (RTSTAMPS_OUT, ["-DSWARM_STAMPS=2"]), "hodrop": (HODROP_OUT, ["-DSWARM_HO_FORCE_DROP=1"])}
 
 
 def build(force: bool = False, verbose: bool = True, stamps: bool = False, variant: str = "main",

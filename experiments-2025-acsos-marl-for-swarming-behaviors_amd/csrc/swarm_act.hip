@@ -256,8 +256,10 @@ int swarm_n_params(void) { return N_PARAMS; }
 // profile's counters only for the library that wrote them
 const char* swarm_build_info(void) {
   return "libswarm_hip gfx950 abi " SWARM_STR(SWARM_ABI_VERSION) " src " SWARM_SRC_DIGEST
-#if SWARM_STAMPS
+#if SWARM_STAMPS == 1
          " stamps"
+#elif SWARM_STAMPS == 2
+         " rtstamps"
 #endif
 #if SWARM_HO_FORCE_DROP
          " hodrop"

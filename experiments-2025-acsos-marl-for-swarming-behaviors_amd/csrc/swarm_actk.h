@@ -74,7 +74,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   float* red = S.red;
   SWARM_RTSTAMP(30);
   SWARM_STAMP(0);
-#if SWARM_STAMPS   // rollouts, slot 29: where the wave runs (HW_ID in the low word, XCC_ID in the high word)
+#if SWARM_STAMPS == 1   // rollouts, slot 29: where the wave runs (HW_ID in the low word, XCC_ID in the high word)
   if (MODE == MODE_ROLLOUT && g_swarm_stamps && (threadIdx.x & 63) == 0)
     g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + 29] =
         (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
@@ -216,7 +216,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
 
   for (int it = 0; it < n_ticks; ++it) {
-#if SWARM_STAMPS   // stamps build: the wave's slowest tick (slot 25 cycles, slot 19 tick index)
+#if SWARM_STAMPS == 1   // stamps build: the wave's slowest tick (slot 25 cycles, slot 19 tick index)
     const long long t_tick0 = clock64();
 #endif
     if (MODE != MODE_Q) {
@@ -432,7 +432,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       if (A.out.hits) A.out.hits[d.gid] = hits_sum;
     }
     wave_lds_sync();   // every lane done with this tick's LDS rows before the next tick rewrites them
-#if SWARM_STAMPS
+#if SWARM_STAMPS == 1
     if (g_swarm_stamps && (threadIdx.x & 63) == 0) {
       unsigned long long* ws = g_swarm_stamps + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32;
       const unsigned long long dt = (unsigned long long)(clock64() - t_tick0);

@@ -249,37 +249,38 @@ __host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (
 __device__ inline float xor32(float v) { return __shfl_xor(v, 32, 64); }
 
 // ---------------------------------------------------------------- diagnostic stamps
-// Built only into the diagnostic library (-DSWARM_STAMPS=1, libswarm_hip_stamps.so):
-// lane 0 of every wave records s_memtime at named points; read their SHARES, never
-// the run time of that build (cdna_hip_programming.md §7 "In-kernel stamps").
+// Built only into the diagnostic libraries; lane 0 of every wave records a clock at named
+// points into the buffer swarm_dbg_stamps_* installs:
+//  - SWARM_STAMPS=1 (libswarm_hip_stamps.so): s_memtime segment stamps (SWARM_STAMP) and the
+//    s_memrealtime launch stamps (SWARM_RTSTAMP); read the SHARES, never that build's run time
+//    (cdna_hip_programming.md §7 "In-kernel stamps");
+//  - SWARM_STAMPS=2 (libswarm_hip_rtstamps.so): the realtime launch stamps only (a few per wave),
+//    for kernel spans and launch boundaries close to the product build's (tools/tick_split_stamps.py).
 #ifndef SWARM_STAMPS
 #define SWARM_STAMPS 0
 #endif
 #if SWARM_STAMPS
 static __constant__ unsigned long long* g_swarm_stamps;
-#define SWARM_STAMP(k)                                                                        \
+#define SWARM_STAMP_AT(k, instr)                                                              \
   do {                                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     unsigned long long _t;                                                                    \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");               \
+    asm volatile(instr " %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     if (g_swarm_stamps && (threadIdx.x & 63) == 0)                                            \
       g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + (k)] = _t;         \
   } while (0)
 // s_memrealtime: the chip-wide 100 MHz clock, comparable across XCDs (launch spans, gaps)
-#define SWARM_RTSTAMP(k)                                                                      \
-  do {                                                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                                        \
-    unsigned long long _t;                                                                    \
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
-    __builtin_amdgcn_sched_barrier(0);                                                        \
-    if (g_swarm_stamps && (threadIdx.x & 63) == 0)                                            \
-      g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + (k)] = _t;         \
-  } while (0)
+#define SWARM_RTSTAMP(k) SWARM_STAMP_AT(k, "s_memrealtime")
+#endif
+#if SWARM_STAMPS == 1
+#define SWARM_STAMP(k) SWARM_STAMP_AT(k, "s_memtime")
 #else
 #define SWARM_STAMP(k) \
   do {              \
   } while (0)
+#endif
+#if !SWARM_STAMPS
 #define SWARM_RTSTAMP(k) \
   do {                \
   } while (0)

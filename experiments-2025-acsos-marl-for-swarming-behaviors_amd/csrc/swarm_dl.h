@@ -366,7 +366,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
   const unsigned long long tb = __ballot(run);
   if (tb != 0ull) {
     // boundary ties: the introselect restatement, G lanes per row
-#if SWARM_STAMPS   // stamps build: per-wave tie-path entries (slot 27) and s_memtime cycles in it (slot 28)
+#if SWARM_STAMPS == 1   // stamps build: per-wave tie-path entries (slot 27) and s_memtime cycles in it (slot 28)
     const long long s0 = clock64();
 #endif
     wave_lds_sync();
@@ -377,7 +377,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
       memo->sig_hi[n] = sig_hi;
       memo->mask[n] = sm.knn[n];
     }
-#if SWARM_STAMPS
+#if SWARM_STAMPS == 1
     wave_lds_sync();
     const long long s1 = clock64();
     if (g_swarm_stamps && lane == 0) {
@@ -388,7 +388,7 @@ __device__ inline void knn_masks_wave(int lane, int N, int k, WSmall<NS>& sm, fl
     }
 #endif
   }
-#if SWARM_STAMPS
+#if SWARM_STAMPS == 1
   if (memo && g_swarm_stamps && lane == 0 && __ballot(hit) != 0ull)   // slot 18: memo hits
     g_swarm_stamps[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 32 + 18] += 1ull;
 #endif

@@ -316,6 +316,83 @@ def reset_centres(scenario: int, n_envs: int, seed: int, episode: int, shared: b
     return torch.tensor(np.stack([cx, cy], axis=1).astype(np.float32))
 
 
+def reset_from_first_step(P0, P1, scenario: int, window: int = 64):
+    """The reset formation an evaluation episode started from, recovered from its first two
+    recorded positions (test infrastructure: the reference re-seeds torch and draws its reset
+    centre from a stream this build cannot reproduce, SURVEY §8(c), but its Simulator records
+    every tick's positions after the step, simulator.py:59-84).
+
+    At reset the agents stand on the generate_grid formation around a centre c with v = 0
+    (go_to_position_scenario.py:52-106, obstacle_avoidance_scenario.py:63-133); the grid spacing
+    (0.15) exceeds the contact distance (0.1) and the obstacle is far, so the first step has no
+    collision force: v1 = dt u0 and P0 = p0 + dt v1.  The centre is unknown, so P0 alone cannot
+    tell a common u0 from a shifted centre; the second step can: (P1 - P0) / dt - dt f(P0) =
+    0.75 dt u0 + dt u1 (VMAS drag 0.25, f the collision force at P0), and 0.075 a + 0.1 b takes a
+    different value for each of the nine level pairs (a, b).  With u0 known, p0 is the fp32 value
+    next to P0 - dt v1 whose first step reproduces P0 exactly (checked with env_step, as is the
+    grid: P0 - dt v1 - offset agrees on one centre).  P0, P1 [N, 2] fp32.
+    Returns (p0 [N, 2] fp32, u0 as actions [N] long)."""
+    P0 = np.asarray(P0, dtype=np.float32)
+    P1 = np.asarray(P1, dtype=np.float32)
+    N = P0.shape[0]
+    f1 = env_step(torch.tensor(P0)[None], torch.zeros(1, N, 2), torch.zeros(1, N, dtype=torch.long),
+                  scenario)["force"][0].double().numpy()                          # action 0: u = 0, force = f(P0)
+    x = (P1.astype(np.float64) - P0.astype(np.float64)) / DT - DT * f1           # 0.075 u0 + 0.1 u1 per axis
+    lv = np.array(ACTION_LEVELS)
+    combos = np.array([[0.75 * DT * a0 + DT * a1 for a1 in lv] for a0 in lv])     # [u0 level][u1 level]
+    lidx = np.zeros((N, 2), dtype=np.int64)
+    for i in range(N):
+        for k in range(2):
+            err = np.abs(combos - x[i, k])
+            j0, j1 = np.unravel_index(int(np.argmin(err)), err.shape)
+            if err[j0, j1] > 1e-3 or np.sort(err.ravel())[1] < 1e-2:
+                raise ValueError("the first two recorded steps do not determine the first action")
+            lidx[i, k] = j0
+    acts = (3 * lidx[:, 0] + lidx[:, 1]).tolist()
+    offs = grid_offsets(N)
+    centres = P0.astype(np.float64) - 0.01 * lv[lidx] - offs
+    if np.abs(centres - centres[0]).max() > 1e-4:
+        raise ValueError("the first recorded positions are not one step from a grid formation")
+    a = torch.tensor(acts, dtype=torch.long)
+    u = decode_actions(a).numpy()
+    step = (u * np.float32(DT)).astype(np.float32) * np.float32(DT)   # vel_new * dt with vel_new = 0 * 0.75 + u * dt
+    p0 = np.empty_like(P0)
+    for i in range(N):
+        for k in range(2):
+            x = np.float32(P0[i, k] - step[i, k])
+            for _ in range(window):   # walk to an fp32 value whose step lands exactly on P0
+                y = np.float32(x + step[i, k])
+                if y == P0[i, k]:
+                    break
+                x = np.nextafter(x, np.float32(np.inf if y < P0[i, k] else -np.inf), dtype=np.float32)
+            p0[i, k] = x
+    p0t = torch.tensor(p0)
+    got = env_step(p0t[None], torch.zeros(1, N, 2), a[None], scenario)["pos"][0]
+    if not torch.equal(got, torch.tensor(P0)):
+        raise ValueError("no fp32 reset formation reproduces the first recorded step")
+    return p0t, a
+
+
+def episode_result(rew, avg_dist, hits):
+    """One result.csv row of an evaluation episode as the reference's Simulator forms it
+    (simulator.py:59-109): Reward = (sum over ticks of the python sum of the agents' fp32
+    rewards) / max_steps, accumulated in fp32 in that order; Collisions = the summed per-tick
+    obstacle hits; Distance (end) / (beginning) = average_distance_to_goal() after the last /
+    the first step.  rew [T, N] fp32 per agent and tick, avg_dist [T], hits [T].
+    Returns (reward, collisions, distance end, distance beginning) as Python floats."""
+    rew = torch.as_tensor(rew, dtype=torch.float32)
+    T, N = rew.shape
+    total = torch.zeros((), dtype=torch.float32)
+    for t in range(T):
+        s = torch.zeros((), dtype=torch.float32)   # sum(rewards.values()) starts from int 0
+        for i in range(N):
+            s = s + rew[t, i]
+        total = total + s
+    avg_dist = torch.as_tensor(avg_dist, dtype=torch.float32)
+    return (float(total / T), float(torch.as_tensor(hits, dtype=torch.float64).sum()), float(avg_dist[-1]),
+            float(avg_dist[0]))
+
+
 # ---------------------------------------------------------------------------
 # observations / node features
 # ---------------------------------------------------------------------------
@@ -700,7 +777,7 @@ def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_sta
     Returns (loss, flat grad [N_PARAMS], online Q at the taken actions, TD targets).
     """
     if conv == "gcn":
-        return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma)
+        return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma, dtype)
     S, N, _ = s_state.shape
     params = {k: v.to(dtype).clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
     tparams = {k: v.to(dtype) for k, v in unflatten_params(flat_target).items()}
@@ -720,15 +797,16 @@ def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_sta
     return float(loss.item()), grad, values.detach().squeeze(1), target
 
 
-def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma):
+def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma,
+                      dtype=torch.float32):
     S, N, _ = s_state.shape
-    params = {k: v.clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
-    tparams = unflatten_params(flat_target)
-    mult = multiplicity_complete(S, N)
-    x = node_features(s_state[..., :2], s_state[..., 2:4])
-    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4])
+    params = {k: v.to(dtype).clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
+    tparams = {k: v.to(dtype) for k, v in unflatten_params(flat_target).items()}
+    mult = multiplicity_complete(S, N).to(dtype)
+    x = node_features(s_state[..., :2], s_state[..., 2:4]).to(dtype)
+    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4]).to(dtype)
     a = actions.reshape(-1).to(torch.long)
-    r = rewards.reshape(-1).to(torch.float32)
+    r = rewards.reshape(-1).to(torch.float32).to(dtype)
     values = gcn_conv_dense(params, x, mult).reshape(S * N, -1).gather(1, a.unsqueeze(1))
     with torch.no_grad():
         next_values = gcn_conv_dense(tparams, xn, mult).reshape(S * N, -1).max(dim=1)[0]

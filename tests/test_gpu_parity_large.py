@@ -1,16 +1,29 @@
-"""The learning half against the oracle at the BASELINE.json sizes (VERDICT r2 "next" #1).
+"""The learning half against the oracle at the BASELINE.json sizes (VERDICT r2 "next" #1, r3 #2/#7).
 
 C2 = GoTo, 8 agents x 1024 envs, TD batch S = 1024 graphs (256 TD blocks, 256 gradient slabs
 summed by the 105-block reduce); C3 = ObstacleAvoidance, 12 agents x 1024 envs, S = 1024 (one
-graph per TD wave).  Both the reference-shaped API sequence (swarm_td_grad -> swarm_grad_reduce
--> swarm_adam_step, train_gcn_dqn.py:112-137) and the headline's fused swarm_train_tick (whose
-TD graphs partly come from the tick's own replay slot through the hand-off records) are
-compared with the oracle's autograd restatement (oracle.swarm_oracle.td_loss_grad / clip_adam)
-on the same replay rows, with replay content from real acting ticks (reset grid, collisions).
+graph per TD wave); C5's shard = ObstacleAvoidance, 5 and 12 agents x 512 envs per GPU, S = 512,
+GAT and the a13 GCNConv variant.  Both the reference-shaped API sequence (swarm_td_grad ->
+swarm_grad_reduce -> swarm_adam_step, train_gcn_dqn.py:112-137) and the headline's fused
+swarm_train_tick (whose TD graphs partly come from the tick's own replay slot through the
+hand-off records) are compared with the oracle's autograd restatement (oracle.swarm_oracle
+td_loss_grad / clip_adam), with replay content from real acting ticks (reset grid, collisions).
 
-Every value is also measured against the same restatement in float64 (the exact value both
-fp32 paths approximate), so the GPU's error is quoted beside the fp32 oracle's own; the
-achieved errors go to parity_errors.json (conftest.record) and are kept under profiles/.
+The sampled rows are not taken on trust: s' and r of every sampled transition are re-derived from
+(s, a) by the oracle's env_step (simulator.py:59-68 / train_gcn_dqn.py:168-172 semantics), checked
+against the GPU's ring, and the oracle's TD runs on the oracle's own s' and r.
+
+Tolerances (fixed before the round-4 measurements; the achieved errors go to
+parity_errors.gpu.json via conftest.record and are kept under profiles/):
+- gradient, per parameter tensor: the GPU's largest distance to the float64 evaluation is at most
+  4x the fp32 oracle's own plus 4 ulps of the tensor's largest element;
+- gradient, per element: within 4x that element's fp32 rounding noise plus 2 ulps of its value,
+  the noise being the largest distance to float64 of three fp32 oracle evaluations that sum the
+  batch in different orders (as given, reversed, shuffled), floored at the tensor's median noise;
+- Adam, isolated from the gradient: m, v and the weights against torch.optim.Adam applied to the
+  GPU's OWN gradient: m within 8 ulps and v within 16 ulps of the magnitude of their update terms
+  (beta * old + (1 - beta) * new), the weights within 4 ulps of max(|w|, lr);
+- end to end, weights after Adam within 2e-6 of torch's update on the fp32 oracle's gradient.
 """
 import pytest
 import torch
@@ -20,7 +33,10 @@ from tests.conftest import assert_close_rel, error_stats, fp32_ulp, record
 
 pytestmark = pytest.mark.gpu
 
-CASES = [("C2", "GoTo", 8, 1024, 1024), ("C3", "ObstacleAvoidance", 12, 1024, 1024)]
+CASES = [("C2", "GoTo", 8, 1024, 1024, "gat"), ("C3", "ObstacleAvoidance", 12, 1024, 1024, "gat"),
+         ("C5 N=5 GAT", "ObstacleAvoidance", 5, 512, 512, "gat"), ("C5 N=12 GAT", "ObstacleAvoidance", 12, 512, 512, "gat"),
+         ("C5 N=5 GCN", "ObstacleAvoidance", 5, 512, 512, "gcn"), ("C5 N=12 GCN", "ObstacleAvoidance", 12, 512, 512, "gcn")]
+SCEN = {"GoTo": O.SCENARIO_GOTO, "ObstacleAvoidance": O.SCENARIO_OA}
 
 
 @pytest.fixture(scope="module")
@@ -44,56 +60,114 @@ def _prefill(eng, slots):
     torch.cuda.synchronize()
 
 
-def _rows(eng, idx):
+def _rows(eng, idx, scen, name):
+    """The sampled transitions (s, a, r, s'): s and a from the ring; s' and r re-derived from them
+    by the oracle's env_step and checked against the ring (positions / velocities within 1e-6,
+    positions bit-exact for agents with no contact force; reward within 1e-6 relative)."""
     B = eng.B
     idx = idx.cpu().long()
     slot, env = idx // B, idx % B
-    return (eng.rep_s.cpu()[slot, env], eng.rep_a.cpu()[slot, env].long(), eng.rep_r.cpu()[slot, env],
-            eng.rep_s1.cpu()[slot, env])
+    s, a = eng.rep_s.cpu()[slot, env], eng.rep_a.cpu()[slot, env].long()
+    r_gpu, s1_gpu = eng.rep_r.cpu()[slot, env], eng.rep_s1.cpu()[slot, env]
+    step = O.env_step(s[..., :2], s[..., 2:], a, SCEN[scen])
+    s1 = torch.cat([step["pos"], step["vel"]], -1)
+    record(f"{name} ring s' vs oracle env_step", error_stats(s1_gpu, s1))
+    assert (s1_gpu - s1).abs().max() <= 1e-6
+    free = step["force"].eq(O.decode_actions(a)).all(-1)
+    assert torch.equal(s1_gpu[..., :2][free], s1[..., :2][free])
+    assert_close_rel(r_gpu, step["rew"], 1e-6, f"{name} ring r vs oracle env_step")
+    return s, a, step["rew"].to(torch.float32), s1
 
 
-def _grad_bound_check(name, g_gpu, g32, g64):
-    """Gradient, per parameter tensor: the GPU's largest distance to the float64 value is at most
-    4x the fp32 oracle's own (torch autograd, the reference's arithmetic) plus 4 fp32 ulps of the
-    tensor's largest element; elementwise, every element is also within 2e-4 of its own magnitude
-    plus 4e-6 of the tensor's largest (the fp32 oracle itself reaches 0.75 of half that bound on
-    conv1.att_dst, whose elements are softmax-backward sums that cancel to rounding noise, so a
-    tighter one would only test which of two valid fp32 summation orders got luckier).  Gradient elements are sums over S*N nodes whose terms
-    cancel, so an element's rounding error scales with its terms, not with its value: both fp32
-    paths sit thousands of ulps of the value away on such elements (profiles/
-    r03_parity_errors_large.json), and an ulp bound on the value alone is meaningless there.
-    Observed (round 3): GPU / oracle ratio <= 2.6 on every tensor of C2 and C3."""
+def oracle_grad_orders(p, t, s, a, r, s1, conv="gat", seed=0, edge_fn=None):
+    """The fp32 oracle's gradient with the batch summed in three orders (as given, reversed,
+    shuffled; each a valid fp32 evaluation of the same sum), and the float64 value.
+    edge_fn(s_graphs) -> Batch edge_index for kNN / radius graphs (None: complete)."""
+    S = s.shape[0]
+    perms = [torch.arange(S), torch.arange(S - 1, -1, -1), torch.randperm(S, generator=torch.Generator().manual_seed(seed))]
+    g32s, loss32 = [], None
+    for q in perms:
+        ei = None if edge_fn is None else edge_fn(s[q])
+        ein = None if edge_fn is None else edge_fn(s1[q])
+        loss, g, _, _ = O.td_loss_grad(p, t, s[q], a[q], r[q], s1[q], edge_index=ei, edge_index_next=ein, conv=conv)
+        g32s.append(g)
+        loss32 = loss if loss32 is None else loss32
+    ei = None if edge_fn is None else edge_fn(s)
+    ein = None if edge_fn is None else edge_fn(s1)
+    loss64, g64, _, _ = O.td_loss_grad(p, t, s, a, r, s1, edge_index=ei, edge_index_next=ein, conv=conv,
+                                       dtype=torch.float64)
+    return loss32, g32s, loss64, g64
+
+
+def _grad_bound_check(name, g_gpu, g32s, g64):
+    """Gradient vs the float64 evaluation (module docstring).  Gradient elements are sums over S*N
+    nodes whose terms cancel, so an element's rounding error scales with its terms, not with its
+    value: both fp32 paths sit thousands of ulps of the value away on such elements, and an ulp
+    bound on the value alone would only test which summation order got luckier.  The per-element
+    bound therefore comes from the fp32 oracle's own noise on that element."""
+    if torch.is_tensor(g32s):
+        g32s = [g32s]
     o = 0
-    worst, worst_ratio, worst_k = 0.0, 0.0, None
+    worst_ratio_t, worst_elem, worst_k = 0.0, 0.0, None
     for k, shape in O.PARAM_ORDER:
         n = 1
         for s in shape:
             n *= s
-        a, b, c = g_gpu[o:o + n].double(), g64[o:o + n], g32[o:o + n].double()
+        a, b = g_gpu[o:o + n].double(), g64[o:o + n]
+        cs = [g[o:o + n].double() for g in g32s]
         gmax = float(b.abs().max())
         floor = 2e-6 * gmax
         st_gpu = error_stats(a, b, scale=floor)
-        st_o32 = error_stats(c, b, scale=floor)
-        bound = 4.0 * st_o32["max_abs"] + 4.0 * float(fp32_ulp(torch.tensor([gmax]))[0])
+        st_o32 = error_stats(cs[0], b, scale=floor)
+        # per tensor: 4x the fp32 oracle's own largest distance + 4 ulps of the largest element
+        o32_max = max(float((c - b).abs().max()) for c in cs)
+        bound = 4.0 * o32_max + 4.0 * float(fp32_ulp(torch.tensor([gmax]))[0])
         record(f"{name} grad[{k}] gpu vs fp64", st_gpu, floor=floor, bound_abs=bound)
         record(f"{name} grad[{k}] oracle32 vs fp64", st_o32, floor=floor)
-        assert st_gpu["max_abs"] <= bound, (name, k, st_gpu["max_abs"], st_o32["max_abs"])
-        worst_ratio = max(worst_ratio, st_gpu["max_abs"] / max(st_o32["max_abs"], 1e-30))
-        elem_bound = 2e-4 * b.abs() + 2.0 * floor
-        excess = ((a - b).abs() - elem_bound).max().item()
-        record(f"{name} grad[{k}] elementwise: largest error / bound", {
-            "gpu": float(((a - b).abs() / elem_bound).max()), "oracle32": float(((c - b).abs() / elem_bound).max())})
-        if excess > worst:
-            worst, worst_k = excess, k
+        assert st_gpu["max_abs"] <= bound, (name, k, st_gpu["max_abs"], o32_max)
+        worst_ratio_t = max(worst_ratio_t, st_gpu["max_abs"] / max(o32_max, 1e-30))
+        # per element: 4x the element's fp32 noise (floored at the tensor's median noise) + 2 ulps
+        noise = torch.stack([(c - b).abs() for c in cs]).max(dim=0).values
+        noise = torch.maximum(noise, noise.median())
+        elem_bound = 4.0 * noise + 2.0 * fp32_ulp(b)
+        ratio = float(((a - b).abs() / elem_bound).max())
+        record(f"{name} grad[{k}] elementwise: largest error / bound", {"gpu": ratio, "n_orders": len(cs)})
+        if ratio > worst_elem:
+            worst_elem, worst_k = ratio, k
         o += n
-    record(f"{name} grad: worst per-tensor ratio gpu/oracle32 error", {"ratio": worst_ratio})
-    assert worst <= 0.0, f"{name}: a {worst_k} gradient element outside 2e-4 rel + 4e-6 x tensor max (excess {worst:.3e})"
+    record(f"{name} grad: worst per-tensor ratio gpu/oracle32 error", {"ratio": worst_ratio_t,
+                                                                       "worst_elementwise_ratio": worst_elem})
+    assert worst_elem <= 1.0, f"{name}: a {worst_k} gradient element outside its bound (ratio {worst_elem:.3f})"
 
 
-def _compare_update(name, eng, p0, t0, m0, v0, step0, idx, S, N):
-    s, a, r, s1 = _rows(eng, idx)
-    loss32, g32, _, _ = O.td_loss_grad(p0, t0, s, a, r, s1)
-    loss64, g64, _, _ = O.td_loss_grad(p0, t0, s, a, r, s1, dtype=torch.float64)
+def _adam_check(name, p_gpu, m_gpu, v_gpu, p0, g_gpu, m0, v0, step0, norm_gpu=None, lr=1e-3, b1=0.9, b2=0.999):
+    """clip_grad_norm_ + Adam of the GPU, isolated from the gradient: against torch on the GPU's
+    OWN gradient (module docstring for the bounds)."""
+    m0 = torch.zeros_like(p0) if m0 is None else m0
+    v0 = torch.zeros_like(p0) if v0 is None else v0
+    ref_p, ref_m, ref_v, ref_norm = O.clip_adam(p0, g_gpu, m0, v0, step0)
+    if norm_gpu is not None:
+        st = error_stats(torch.tensor([norm_gpu]), torch.tensor([ref_norm]))
+        record(f"{name} clip total_norm (own gradient)", st)
+        assert st["max_ulp"] <= 8, st
+    coef = min(1.0, 1.0 / (ref_norm + 1e-6))
+    gc = g_gpu.double() * coef
+    m_terms = b1 * m0.double().abs() + (1 - b1) * gc.abs()
+    v_terms = b2 * v0.double().abs() + (1 - b2) * gc * gc
+    st_m = error_stats(m_gpu, ref_m, scale=m_terms)
+    st_v = error_stats(v_gpu, ref_v, scale=v_terms)
+    st_p = error_stats(p_gpu, ref_p, scale=torch.full_like(p_gpu, lr, dtype=torch.float64))
+    record(f"{name} adam m (own gradient)", st_m, tol_ulp=8)
+    record(f"{name} adam v (own gradient)", st_v, tol_ulp=16)
+    record(f"{name} weights after Adam (own gradient)", st_p, tol_ulp=4)
+    assert st_m["max_ulp"] <= 8, st_m
+    assert st_v["max_ulp"] <= 16, st_v
+    assert st_p["max_ulp"] <= 4, st_p
+
+
+def _compare_update(name, eng, p0, t0, idx, S, N, scen, conv):
+    s, a, r, s1 = _rows(eng, idx, scen, name)
+    loss32, g32s, loss64, g64 = oracle_grad_orders(p0, t0, s, a, r, s1, conv=conv, seed=S + N)
     grad = eng.grad.cpu()
     loss = grad[O.N_PARAMS].double().item() / (S * N)
     # TD loss: north_star 1e-5 vs the fp32 oracle, and in ulps vs fp64: within 4x the fp32
@@ -104,59 +178,49 @@ def _compare_update(name, eng, p0, t0, m0, v0, step0, idx, S, N):
     record(f"{name} TD loss gpu vs fp64", st_gpu)
     record(f"{name} TD loss oracle32 vs fp64", st_o32)
     assert st_gpu["max_ulp"] <= 4.0 * st_o32["max_ulp"] + 8.0, (st_gpu, st_o32)
-    _grad_bound_check(name, grad[:O.N_PARAMS], g32, g64)
-    return g32
+    _grad_bound_check(name, grad[:O.N_PARAMS], g32s, g64)
+    return g32s[0], grad[:O.N_PARAMS].clone()
 
 
-def _compare_adam(name, eng, p0, m0, v0, step0, g32):
-    ref_p, ref_m, ref_v, ref_norm = O.clip_adam(p0, g32, m0, v0, step0)
-    c = eng.read_ctrl()
-    assert c["adam_step"] == step0 + 1
-    assert_close_rel(c["grad_norm"], ref_norm, 1e-5, f"{name} clip total_norm")
-    record(f"{name} clip total_norm ulp", error_stats(torch.tensor([c["grad_norm"]]), torch.tensor([ref_norm])))
-    assert ref_norm > 1.0 or step0 > 0, "the clip must be active at these sizes (norm > max_norm)"
-    p, m, v = eng.params.cpu(), eng.adam_m.cpu(), eng.adam_v.cpu()
-    st = error_stats(p, ref_p)
-    record(f"{name} params after Adam", st)
+def _end_to_end_weights(name, p_gpu, p0, g32, m0, v0, step0):
+    """weights after Adam vs torch's update on the fp32 oracle's gradient (2e-6 absolute)."""
+    ref_p, _, _, ref_norm = O.clip_adam(p0, g32, torch.zeros_like(p0) if m0 is None else m0,
+                                        torch.zeros_like(p0) if v0 is None else v0, step0)
+    st = error_stats(p_gpu, ref_p)
+    record(f"{name} weights after Adam vs the oracle-gradient update", st)
     assert st["max_abs"] < 2e-6, st
-    # m = (1 - b1) * coef * g: its ulp error carries the clip coefficient's (v_sqrt_f32 + rcp
-    # in the kernel vs torch's correctly rounded max_norm / (norm + 1e-6))
-    record(f"{name} adam m", error_stats(m, ref_m))
-    record(f"{name} adam v", error_stats(v, ref_v))
-    assert_close_rel(m, ref_m, 1e-4, f"{name} adam m")
-    assert_close_rel(v, ref_v, 1e-4, f"{name} adam v")
-    if step0 == 0:
-        g = eng.grad.cpu()[:O.N_PARAMS].double()
-        sel = g.abs() > 1e-3 * g.abs().max()
-        coef_gpu = (m.double()[sel] / (0.1 * g[sel])).median().item()
-        coef_ref = float(torch.tensor(1.0, dtype=torch.float32) / (torch.tensor(ref_norm, dtype=torch.float32) + 1e-6))
-        record(f"{name} clip coefficient (from m / (0.1 g))",
-               error_stats(torch.tensor([coef_gpu]), torch.tensor([coef_ref])))
+    return ref_norm
 
 
-@pytest.mark.parametrize("name,scen,N,B,S", CASES)
-def test_td_api_update_at_benchmark_size(sw, golden_weights, name, scen, N, B, S):
+@pytest.mark.parametrize("name,scen,N,B,S,conv", CASES)
+def test_td_api_update_at_benchmark_size(sw, golden_weights, name, scen, N, B, S, conv):
     """swarm_td_grad + swarm_grad_reduce + swarm_adam_step (the reference-shaped
-    train_step_dqn) on S = 1024 graphs drawn from a 4-slot ring of real transitions."""
+    train_step_dqn) on S graphs drawn from a 4-slot ring of real transitions."""
     slots = 4
     p = _weights(golden_weights, scen, 5)
     tgt = _weights(golden_weights, scen, 6)
     eng = sw.SwarmEngine(scen, N, B, seed=12, params=p, batch=S, replay_capacity=slots * B, eps=0.3,
-                         update_target_every=100000)
+                         update_target_every=100000, conv=conv)
     _prefill(eng, slots)
     eng.target.copy_(tgt.cuda())
     idx = torch.randperm(slots * B, generator=torch.Generator().manual_seed(S + N))[:S].to(torch.int32)
     p0, t0 = eng.params.cpu().clone(), eng.target.cpu().clone()
     eng.td_grad(sample_in=idx.cuda())
     torch.cuda.synchronize()
-    g32 = _compare_update(name, eng, p0, t0, None, None, 0, idx, S, N)
+    g32, g_gpu = _compare_update(name, eng, p0, t0, idx, S, N, scen, conv)
     eng.adam()
     torch.cuda.synchronize()
-    _compare_adam(name, eng, p0, torch.zeros_like(p0), torch.zeros_like(p0), 0, g32)
+    c = eng.read_ctrl()
+    assert c["adam_step"] == 1
+    ref_norm = _end_to_end_weights(name, eng.params.cpu(), p0, g32, None, None, 0)
+    assert ref_norm > 1.0, "the clip must be active at these sizes (norm > max_norm)"
+    assert_close_rel(c["grad_norm"], ref_norm, 1e-5, f"{name} clip total_norm")
+    _adam_check(name, eng.params.cpu(), eng.adam_m.cpu(), eng.adam_v.cpu(), p0, g_gpu, None, None, 0,
+                norm_gpu=c["grad_norm"])
 
 
-@pytest.mark.parametrize("name,scen,N,B,S", CASES)
-def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, B, S):
+@pytest.mark.parametrize("name,scen,N,B,S,conv", CASES)
+def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, B, S, conv):
     """The headline launch (swarm_train_tick + swarm_reduce_advance) at its benchmarked size:
     two consecutive training ticks.  The first tick's gradient (from the initial weights) and
     the second's (after the first's deferred clip + Adam, applied in the second launch's
@@ -165,11 +229,11 @@ def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, 
     slots = 3
     p = _weights(golden_weights, scen, 5)
     eng = sw.SwarmEngine(scen, N, B, seed=13, params=p, batch=S, replay_capacity=(slots + 2) * B, eps=0.3,
-                         update_target_every=100000)
+                         update_target_every=100000, conv=conv)
     assert eng.fused
     _prefill(eng, slots)
     target = eng.target.cpu().clone()
-    prev = None   # clip_adam arguments of the previous tick: (weights, fp32-oracle gradient, m, v, step)
+    prev = None   # (weights, fp32-oracle gradient, GPU gradient, m, v, step) of the previous tick
     for t in range(2):
         ws = eng.read_ctrl()["write_slot"]
         eng.train_tick(full_out=False)
@@ -179,24 +243,19 @@ def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, 
         # the reduce copied them to the current rows
         p_used, m_used, v_used = eng.params.cpu().clone(), eng.adam_m.cpu().clone(), eng.adam_v.cpu().clone()
         if prev is not None:
-            ref_p, ref_m, ref_v, _ = O.clip_adam(*prev)
-            st = error_stats(p_used, ref_p)
-            record(f"{name} fused tick {t}: weights after the deferred step", st)
-            assert st["max_abs"] < 2e-6, st
-            assert_close_rel(m_used, ref_m, 1e-4, f"{name} fused tick {t}: adam m")
-            assert_close_rel(v_used, ref_v, 1e-4, f"{name} fused tick {t}: adam v")
+            pw, g32p, ggp, mp, vp, sp = prev
+            _end_to_end_weights(f"{name} fused tick {t}", p_used, pw, g32p, mp, vp, sp)
+            _adam_check(f"{name} fused tick {t}", p_used, m_used, v_used, pw, ggp, mp, vp, sp)
         idx = eng.samples.cpu().clone()
         assert len(set(idx.tolist())) == S
         n_cur = int(((idx.long() // B) == ws).sum())
         assert n_cur > 0, "some graphs come from the tick's own slot"
         record(f"{name} fused tick {t}: graphs from the tick's own slot", {"n": n_cur})
-        g32 = _compare_update(f"{name} fused tick {t}", eng, p_used, target, None, None, t, idx, S, N)
-        prev = (p_used, g32, m_used, v_used, t)
+        g32, g_gpu = _compare_update(f"{name} fused tick {t}", eng, p_used, target, idx, S, N, scen, conv)
+        prev = (p_used, g32, g_gpu, m_used, v_used, t)
     eng.flush()
     torch.cuda.synchronize()
-    ref_p, ref_m, ref_v, _ = O.clip_adam(*prev)
-    st = error_stats(eng.params.cpu(), ref_p)
-    record(f"{name} fused: weights after the flushed second step", st)
-    assert st["max_abs"] < 2e-6, st
-    assert_close_rel(eng.adam_m.cpu(), ref_m, 1e-4, f"{name} fused adam m after two steps")
-    assert_close_rel(eng.adam_v.cpu(), ref_v, 1e-4, f"{name} fused adam v after two steps")
+    pw, g32p, ggp, mp, vp, sp = prev
+    _end_to_end_weights(f"{name} fused flushed second step", eng.params.cpu(), pw, g32p, mp, vp, sp)
+    _adam_check(f"{name} fused flushed second step", eng.params.cpu(), eng.adam_m.cpu(), eng.adam_v.cpu(), pw, ggp,
+                mp, vp, sp)
