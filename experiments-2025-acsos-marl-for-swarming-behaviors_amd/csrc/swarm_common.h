@@ -235,19 +235,6 @@ __device__ inline void pair_force(float dx, float dy, float& fx, float& fy) {
 // discrete action a in 0..8 -> u = (L[a/3], L[a%3]), L = {0, -1, +1}  
 __host__ __device__ inline float action_level(int l) { return l == 0 ? 0.0f : (l == 1 ? -1.0f : 1.0f); }
 
-// ---------------------------------------------------------------- MFMA (f32 in / f32 acc)
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-// D = A(32xK=2) * B(2x32) + C ; lane l supplies A[l&31][l>>5] and B[l>>5][l&31];
-// D element r of lane l is D[row=(r&3)+8(r>>2)+4(l>>5)][col=l&31].  Bit-exact k-ordered fmaf chain.
-__device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-// row index of accumulator register r in lane half h ("acc layout")
-__host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-
-__device__ inline float xor32(float v) { return __shfl_xor(v, 32, 64); }
-
 // ---------------------------------------------------------------- diagnostic stamps
 // Built only into the diagnostic libraries; lane 0 of every wave records a clock at named
 // points into the buffer swarm_dbg_stamps_* installs:

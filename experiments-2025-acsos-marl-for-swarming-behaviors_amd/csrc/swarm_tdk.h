@@ -12,7 +12,7 @@
 //   GAT: g_uv = dOut_v.h_u ; de_uv = c_uv (g_uv - sum_w c_wv g_wv) ; dp = de * leaky'(p)
 //        da_dst[v] = sum_u dp_uv ; da_src[u] = sum_v dp_uv ; dh_u = sum_v c_uv dOut_v + da_src att_src + da_dst att_dst
 // Parameter sums over the block's 32 node rows: dW1 = dZ^T T, dW2 = dQ^T R, dW = dh^T X on
-// MFMA (32x32x2 f32, node index as K), vectors by LDS column sums; each block writes one
+// MFMA (16x16x4 f32 tiles, node index as K), vectors by LDS column sums; each block writes one
 // slab [N_PARAMS + 1] (last = sum of squared TD errors) and swarm_grad_reduce sums the
 // slabs in a fixed order (bitwise run-to-run reproducible).
 #pragma once
@@ -25,8 +25,8 @@ namespace swarm {
 // ONLINE network on graph w (forward on s with activations kept, dQ, backward of the
 // per-node vectors); wave GPB + w runs the TARGET network on s' of graph w
 // (y = r + gamma max_a Q_tgt), then shares the parameter products.  The parameter
-// gradient of the block is a sum over its 32 node rows: MFMA 32x32x2 f32 with the
-// node index as K, jobs spread over the waves, each writing its slice of the slab.
+// gradient of the block is a sum over its 32 node rows: MFMA 16x16x4 f32 tiles with the
+// node index as K, spread over the waves, each writing its slice of the slab.
 constexpr int kTdRows = 32;
 
 template <int NS>
@@ -76,21 +76,6 @@ struct TdArgs {
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
 // measured against nt (td 8.4 vs 8.0 us) and write-through sc1 (9.5 us) stores.
 __device__ inline void slab_st(float* p, float v) { *p = v; }
-
-// D[i][j] = sum_node A_img[node][i] * B_img[node][j] over the 32 node rows (MFMA, K = node)
-// (all 32 operands read first: no LDS round trip between two steps of the MFMA chain)
-__device__ inline f32x16 mfma_nodesum(const float (*Aimg)[kRow], const float (*Bimg)[kRow], int lane) {
-  const int h = lane >> 5, c = lane & 31;
-  float a[16], b[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) { a[s] = Aimg[2 * s + h][c]; b[s] = Bimg[2 * s + h][c]; }
-#pragma unroll
-  for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(a[s]), "+v"(b[s]));
-  f32x16 acc = {};
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma32(a[s], b[s], acc);
-  return acc;
-}
 
 // NS node slots per wave holding NS / GS graphs of GS slots (GS = 8 < NS = 16 packs two
 // N <= 8 graphs into one wave: every MFMA column is a real node, one wave per SIMD).
@@ -563,36 +548,44 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   int np_pre = 0;   // online waves of this block on the pre path
 #pragma unroll
   for (int w2 = 0; w2 < GPB; ++w2) np_pre += TB.prew[w2];
-  // the parameter products that need only B2's images (each writes its slice of the slab)
-  auto b2_job = [&](int job) {
-    const int col = lane & 31, h = lane >> 5;
-    if (job == 0) {
-      const f32x16 dW1 = mfma_nodesum(TB.dZ, TB.T, lane);
+  // the parameter products that need only B2's images (each writes its slice of the slab).
+  // dW1 = dZ^T T and dW2 = onehot(a) gq R as 16x16x4 MFMA tiles, K = 4 of the block's 32 node
+  // rows per step: dW1 tiles (ti, tj) = jobs 2 ti + tj, dW2's 9 action rows in one 16-row tile
+  // per column half tj = jobs 4 + tj.  A wave runs three tiles of one column half tj, their
+  // chains interleaved with every operand read first (as conditional reads they became a branch
+  // and an LDS round trip in front of each MFMA): 24 MFMAs of 32 cycles where the 32x32x2 form
+  // had 16 of 64 per product, and dW2 takes 16 rows of work instead of 32.
+  auto b2_tiles = [&](int tj) {   // lane (c, p) of the D layout: column c, k-slot / row group p
+    float a1[2][8], b1[8], a2[8], b2v[8];
+    int an[8];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sst(OFF_W1 + acc_row(r, h) * kHidden + col, dW1[r]);
-    } else if (job == 1) {
-      // every operand read up front: as `act == col ? gq : 0` the gq read became a branch
-      // around a masked load per step, an LDS round trip in front of each of the 16 MFMAs
-      int an[16];
-      float gn[16], rn[16];
+    for (int s = 0; s < 8; ++s) {
+      const int n = 4 * s + p;
+      a1[0][s] = TB.dZ[n][c];
+      a1[1][s] = TB.dZ[n][16 + c];
+      b1[s] = TB.T[n][16 * tj + c];
+      b2v[s] = TB.R[n][16 * tj + c];
+      an[s] = TB.act[n];
+      a2[s] = TB.gq[n];
+    }
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int n = 2 * s + h;
-        an[s] = TB.act[n];
-        gn[s] = TB.gq[n];
-        rn[s] = TB.R[n][col];
-      }
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
+    f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 16; ++s) asm volatile("" : "+v"(gn[s]));   // loaded unconditionally
-      f32x16 dW2 = {};
+    for (int s = 0; s < 8; ++s) {
+      d0 = mfma16(a1[0][s], b1[s], d0);
+      d1 = mfma16(a1[1][s], b1[s], d1);
+      d2 = mfma16(an[s] == c ? a2[s] : 0.0f, b2v[s], d2);
+    }
 #pragma unroll
-      for (int s = 0; s < 16; ++s) dW2 = mfma32(an[s] == col ? gn[s] : 0.0f, rn[s], dW2);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int a = acc_row(r, h);
-        if (a < kActions) sst(OFF_W2 + a * kHidden + col, dW2[r]);
-      }
-    } else if (job == 2) {
+    for (int r = 0; r < 4; ++r) {
+      sst(OFF_W1 + (4 * p + r) * kHidden + 16 * tj + c, d0[r]);
+      sst(OFF_W1 + (16 + 4 * p + r) * kHidden + 16 * tj + c, d1[r]);
+      if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
+    }
+  };
+  auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
+    if (job == 2) {
       if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
@@ -772,12 +765,12 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     }
     SWARM_STAMP(27);
   } else {
-    // ---- target waves: products that need only B2's images
-    //      job 0: dW1 = dZ^T T ; job 1: dW2 = onehot(a) gq R ; job 2: db1 ; job 3: db2, loss.
-    //      The vector sums (2, 3) go to the block's pre-path online waves when it has any: theirs
-    //      is the short side of B2 -> B3 there, and the target waves' products the long one
-    for (int job = wi; job < 4; job += GPB)
-      if (job < 2 || np_pre == 0) b2_job(job);
+    // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
+    //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
+    //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
+    for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
+    if (np_pre == 0)
+      for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
   }
   if (online && pre) {   // (GPB = 2: one pre wave takes both sums, two split them)
     if (np_pre == 1 || wi == 0) b2_job(2);
