@@ -41,9 +41,9 @@ struct ReduceArgs {
 
 // 1024 threads = 16 columns x 64 slab groups (105 column blocks: the 1.7 MB of freshly
 // written slabs is read by many CUs at once, 16 KB each); group g sums a contiguous run of
-// slabs with every load issued before the ordered adds, then the 64 group sums of a column
-// are added in a fixed two-level order (8 runs of 8, then the 8 run sums): bitwise
-// reproducible run to run.  Advance mode adds one control block (the last): it prepares
+// slabs with every load issued before the adds, then the 64 group sums of a column are added
+// in a fixed two-level order (8 runs of 8, then the 8 run sums), every level a pairwise tree
+// (tree_sum, swarm_tdk.h): bitwise reproducible run to run.  Advance mode adds one control block (the last): it prepares
 // and stores the whole ctrl update (Adam scalars of the next step in double, the next
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
 // Three more blocks copy w / m / v _nxt -> _cur (one array each), beside the column blocks.
@@ -151,16 +151,13 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
     v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[slab_index(col, b0 + j, n_slabs)] : 0.0f;
-  float s = v0[0];
-#pragma unroll
-  for (int j = 1; j < kChunk; ++j) s = s + v0[j];
+  float s = tree_sum(v0);
   if (col <= N_PARAMS) {
     for (int b = b0 + kChunk; b < b1; b += kChunk) {
       float v[kChunk];
 #pragma unroll
       for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? slabs[slab_index(col, b + j, n_slabs)] : 0.0f;
-#pragma unroll
-      for (int j = 0; j < kChunk; ++j) s = s + v[j];
+      s = s + tree_sum(v);
     }
   }
   SWARM_STAMP(29);
@@ -168,16 +165,17 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   __syncthreads();
   SWARM_STAMP(30);
   if (q < kRedRuns) {
-    float r = part[8 * q][c];
+    float r[8];
 #pragma unroll
-    for (int gi = 1; gi < 8; ++gi) r = r + part[8 * q + gi][c];
-    part2[q][c] = r;
+    for (int gi = 0; gi < 8; ++gi) r[gi] = part[8 * q + gi][c];
+    part2[q][c] = tree_sum(r);
   }
   __syncthreads();
   if (q == 0 && col <= N_PARAMS) {
-    float tot = part2[0][c];
+    float t8[kRedRuns];
 #pragma unroll
-    for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
+    for (int gi = 0; gi < kRedRuns; ++gi) t8[gi] = part2[gi][c];
+    const float tot = tree_sum(t8);
     if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
     else A.grad[col] = tot;
     // this rank's loss of the update (0 when skipped: the TD launch wrote zero slabs)

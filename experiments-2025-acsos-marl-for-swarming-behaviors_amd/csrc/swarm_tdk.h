@@ -29,6 +29,20 @@ namespace swarm {
 // node index as K, spread over the waves, each writing its slice of the slab.
 constexpr int kTdRows = 32;
 
+// pairwise (tree) sum of K values: each term passes log2(K) roundings instead of up to K - 1 in a
+// sequential sum.  The parameter-gradient elements are sums whose terms cancel, so their fp32
+// error scales with the roundings each term passes (tests/test_gpu_parity_large.py bounds it
+// against the fp32 oracle's own noise per element)
+template <int K>
+__device__ inline float tree_sum(float (&v)[K]) {
+  static_assert((K & (K - 1)) == 0, "power of two");
+#pragma unroll
+  for (int w = K / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int i = 0; i < w; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+  return v[0];
+}
+
 template <int NS>
 struct TdLds {
   static constexpr int GPB = kTdRows / NS;
@@ -590,29 +604,21 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
-        float acc = v[0];
-#pragma unroll
-        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        sst(OFF_B1 + lane, acc);
+        sst(OFF_B1 + lane, tree_sum(v));
       }
-    } else if (lane < kActions || lane == 63) {   // db2 / loss: the ordered sum over the 32 rows,
-      // 8 rows' reads at a time (each read unconditional: as selects around the reads they became
-      // a branch and an LDS round trip per row)
-      float acc = 0.0f;
+    } else if (lane < kActions || lane == 63) {   // db2 / loss: the tree sum over the 32 rows (every
+      // read unconditional: as selects around the reads they became a branch and an LDS round
+      // trip per row)
+      int an[kTdRows];
+      float gn[kTdRows], dn[kTdRows];
 #pragma unroll
-      for (int k = 0; k < kTdRows; k += 8) {
-        int a8[8];
-        float g8[8], d8[8];
+      for (int n = 0; n < kTdRows; ++n) { an[n] = TB.act[n]; gn[n] = TB.gq[n]; dn[n] = TB.d2[n]; }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { a8[j] = TB.act[k + j]; g8[j] = TB.gq[k + j]; d8[j] = TB.d2[k + j]; }
+      for (int n = 0; n < kTdRows; ++n) asm volatile("" : "+v"(gn[n]), "+v"(dn[n]));
+      float v[kTdRows];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(g8[j]), "+v"(d8[j]));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = lane == 63 ? d8[j] : (a8[j] == lane ? g8[j] : 0.0f);
-          acc = (k == 0 && j == 0) ? v : acc + v;
-        }
-      }
+      for (int n = 0; n < kTdRows; ++n) v[n] = lane == 63 ? dn[n] : (an[n] == lane ? gn[n] : 0.0f);
+      const float acc = tree_sum(v);
       sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
     }
   };
@@ -808,18 +814,12 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
-        float acc = v[0];
-#pragma unroll
-        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, acc);
+        sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, tree_sum(v));
       } else if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = TB.dO[n][lane];
-        float acc = v[0];
-#pragma unroll
-        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-        sst(OFF_BIAS + lane, acc);
+        sst(OFF_BIAS + lane, tree_sum(v));
       }
     }
   }
