@@ -17,9 +17,12 @@ Tolerances (fixed before the round-4 measurements; the achieved errors go to
 parity_errors.gpu.json via conftest.record and are kept under profiles/):
 - gradient, per parameter tensor: the GPU's largest distance to the float64 evaluation is at most
   4x the fp32 oracle's own plus 4 ulps of the tensor's largest element;
-- gradient, per element: within 4x that element's fp32 rounding noise plus 2 ulps of its value,
-  the noise being the largest distance to float64 of three fp32 oracle evaluations that sum the
-  batch in different orders (as given, reversed, shuffled), floored at the tensor's median noise;
+- gradient, per element: within 1e-4 of the element's magnitude plus 2e-6 of the tensor's largest
+  element (the pre-round-3 bound, restored; round 3 had doubled it to admit a summation-order
+  change).  The oracle is also evaluated with the batch summed in three orders (as given,
+  reversed, shuffled); the largest distance of the three sets the per-tensor bound, and the GPU's
+  error over that per-element order noise is recorded (not asserted: the terms are the same in
+  every order, so it leaves out the per-term rounding an independent evaluation has);
 - Adam, isolated from the gradient: m, v and the weights against torch.optim.Adam applied to the
   GPU's OWN gradient: m within 8 ulps and v within 16 ulps of the magnitude of their update terms
   (beta * old + (1 - beta) * new), the weights within 4 ulps of max(|w|, lr);
@@ -103,8 +106,7 @@ def _grad_bound_check(name, g_gpu, g32s, g64):
     """Gradient vs the float64 evaluation (module docstring).  Gradient elements are sums over S*N
     nodes whose terms cancel, so an element's rounding error scales with its terms, not with its
     value: both fp32 paths sit thousands of ulps of the value away on such elements, and an ulp
-    bound on the value alone would only test which summation order got luckier.  The per-element
-    bound therefore comes from the fp32 oracle's own noise on that element."""
+    bound on the value alone would only test which summation order got luckier."""
     if torch.is_tensor(g32s):
         g32s = [g32s]
     o = 0
@@ -126,18 +128,24 @@ def _grad_bound_check(name, g_gpu, g32s, g64):
         record(f"{name} grad[{k}] oracle32 vs fp64", st_o32, floor=floor)
         assert st_gpu["max_abs"] <= bound, (name, k, st_gpu["max_abs"], o32_max)
         worst_ratio_t = max(worst_ratio_t, st_gpu["max_abs"] / max(o32_max, 1e-30))
-        # per element: 4x the element's fp32 noise (floored at the tensor's median noise) + 2 ulps
+        # per element: the pre-round-3 bound, 1e-4 of the element's own magnitude plus 2e-6 of the
+        # tensor's largest (the round-3 doubling is withdrawn)
+        elem_bound = 1e-4 * b.abs() + floor
+        ratio = float(((a - b).abs() / elem_bound).max())
+        # diagnostic only (not asserted): the GPU's error against the fp32 oracle's own per-element
+        # noise over its summation orders (the terms themselves are identical in every order, so
+        # this underestimates the noise of an evaluation that also computes the terms differently)
         noise = torch.stack([(c - b).abs() for c in cs]).max(dim=0).values
         noise = torch.maximum(noise, noise.median())
-        elem_bound = 4.0 * noise + 2.0 * fp32_ulp(b)
-        ratio = float(((a - b).abs() / elem_bound).max())
-        record(f"{name} grad[{k}] elementwise: largest error / bound", {"gpu": ratio, "n_orders": len(cs)})
+        record(f"{name} grad[{k}] elementwise: largest error / bound", {
+            "gpu": ratio, "oracle32": float(((cs[0] - b).abs() / elem_bound).max()),
+            "gpu_over_oracle_order_noise": float(((a - b).abs() / (4.0 * noise + 2.0 * fp32_ulp(b))).max())})
         if ratio > worst_elem:
             worst_elem, worst_k = ratio, k
         o += n
     record(f"{name} grad: worst per-tensor ratio gpu/oracle32 error", {"ratio": worst_ratio_t,
                                                                        "worst_elementwise_ratio": worst_elem})
-    assert worst_elem <= 1.0, f"{name}: a {worst_k} gradient element outside its bound (ratio {worst_elem:.3f})"
+    assert worst_elem <= 1.0, f"{name}: a {worst_k} gradient element outside 1e-4 rel + 2e-6 x tensor max (ratio {worst_elem:.3f})"
 
 
 def _adam_check(name, p_gpu, m_gpu, v_gpu, p0, g_gpu, m0, v0, step0, norm_gpu=None, lr=1e-3, b1=0.9, b2=0.999):
