@@ -48,7 +48,8 @@ class SwarmActOut(ctypes.Structure):
 class SwarmAdamCfg(ctypes.Structure):
     _fields_ = [("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float),
                 ("max_norm", c_float), ("gamma", c_float), ("batch", c_int32),
-                ("update_target_every", c_int32), ("world_size", c_int32), ("pad", c_int32)]
+                ("update_target_every", c_int32), ("world_size", c_int32), ("pad", c_int32),
+                ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double), ("beta2_d", ctypes.c_double)]
 
 
 class SwarmLearner(ctypes.Structure):

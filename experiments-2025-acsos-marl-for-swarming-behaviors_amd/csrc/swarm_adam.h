@@ -33,6 +33,14 @@ __device__ inline void ctrl_set_double(swarm_ctrl* c, int word, double v) {
 constexpr int CTRL_B1POW = 0;   // beta_pow[0..1] = beta1^adam_step
 constexpr int CTRL_B2POW = 2;   // beta_pow[2..3] = beta2^adam_step
 
+// the hyper-parameters in double as torch.optim.Adam holds them (swarm_adam_cfg *_d; 0 = the
+// float field): torch forms 1 - beta1 = 0.1, 1 - beta2 = 0.001 and the bias corrections from
+// Python floats, and (float)(1 - (double)0.999f) is 1.3e-5 away from 0.001f, a systematic
+// 200-ulp bias on v
+__device__ inline double adam_lr(const swarm_adam_cfg& hp) { return hp.lr_d != 0.0 ? hp.lr_d : (double)hp.lr; }
+__device__ inline double adam_beta1(const swarm_adam_cfg& hp) { return hp.beta1_d != 0.0 ? hp.beta1_d : (double)hp.beta1; }
+__device__ inline double adam_beta2(const swarm_adam_cfg& hp) { return hp.beta2_d != 0.0 ? hp.beta2_d : (double)hp.beta2; }
+
 // Adam scalars of the step after the one ctrl's beta powers describe (torch single_tensor:
 // step_size = lr / bias_correction1, bias_correction2_sqrt = sqrt(bias_correction2), both
 // in double), stored in ctrl as floats by whoever advances the powers, so the optimizer
@@ -40,9 +48,9 @@ constexpr int CTRL_B2POW = 2;   // beta_pow[2..3] = beta2^adam_step
 // b1pow / b2pow: beta^s after s steps -> the scalars of step s + 1
 __device__ inline void adam_next_scalars(const swarm_adam_cfg& hp, double b1pow, double b2pow, float& step_size,
                                          float& inv_bc2) {
-  const double b1n = b1pow * (double)hp.beta1;
-  const double b2n = b2pow * (double)hp.beta2;
-  step_size = (float)((double)hp.lr / (1.0 - b1n));
+  const double b1n = b1pow * adam_beta1(hp);
+  const double b2n = b2pow * adam_beta2(hp);
+  step_size = (float)(adam_lr(hp) / (1.0 - b1n));
   inv_bc2 = 1.0f / (float)sqrt(1.0 - b2n);
 }
 __device__ inline void ctrl_store_next_scalars(swarm_ctrl* c, const swarm_adam_cfg& hp) {
@@ -147,8 +155,8 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float 
   const float coef = hp.max_norm * __builtin_amdgcn_rcpf(total_norm + 1e-6f);
   const float clamped = coef < 1.0f ? coef : 1.0f;
   const float bc2_sqrt = inv_bc2_sqrt;   // reciprocal of sqrt(bias_correction2)
-  const float one_m_b1 = (float)(1.0 - (double)hp.beta1);
-  const float one_m_b2 = (float)(1.0 - (double)hp.beta2);
+  const float one_m_b1 = (float)(1.0 - adam_beta1(hp));
+  const float one_m_b2 = (float)(1.0 - adam_beta2(hp));
 #pragma unroll
   for (int j = 0; j < kAdamNJ; ++j) {
     float4 g = R.g[j], w = R.w[j], m = R.m[j], v = R.v[j];

@@ -78,8 +78,8 @@ __device__ inline void red_control(swarm_ctrl* C, const RedCtrl& A) {
     b1p = ctrl_get_double(C, CTRL_B1POW);
     b2p = ctrl_get_double(C, CTRL_B2POW);
     if (c_trained) {   // the step this tick's act kernel applied
-      b1p = b1p * (double)A.hp.beta1;
-      b2p = b2p * (double)A.hp.beta2;
+      b1p = b1p * adam_beta1(A.hp);
+      b2p = b2p * adam_beta2(A.hp);
       adam_next_scalars(A.hp, b1p, b2p, next_step_size, next_inv_bc2);
     }
   } else if (t == 64) {
@@ -239,8 +239,8 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
     if (train) {
       C->adam_step = step;
       C->grad_norm = gn;
-      ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * (double)A.hp.beta1);
-      ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * (double)A.hp.beta2);
+      ctrl_set_double(C, CTRL_B1POW, ctrl_get_double(C, CTRL_B1POW) * adam_beta1(A.hp));
+      ctrl_set_double(C, CTRL_B2POW, ctrl_get_double(C, CTRL_B2POW) * adam_beta2(A.hp));
       ctrl_store_next_scalars(C, A.hp);
     }
     if (A.flush) {

@@ -132,8 +132,9 @@ class SwarmEngine:
         if peer is not None and peer.world_size != world_size:
             raise ValueError(f"peer exchange of {peer.world_size} ranks for world_size {world_size}")
         self.peer = peer
+        # the double fields: torch.optim.Adam's Python-float lr / betas (1 - beta, bias corrections)
         self.hp = SwarmAdamCfg(lr, betas[0], betas[1], adam_eps, max_norm, gamma, self.batch,
-                               update_target_every, world_size, 0)
+                               update_target_every, world_size, 0, float(lr), float(betas[0]), float(betas[1]))
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         # [B][N][4] pos.xy, vel.xy; Flocking keeps its per-agent previous_distance_to_agents after

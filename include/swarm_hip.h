@@ -128,6 +128,10 @@ typedef struct swarm_adam_cfg {
   int32_t update_target_every;   /* 200 at train_gcn_dqn.py:175                   */
   int32_t world_size;            /* ranks whose gradients are summed (grad /= W)   */
   int32_t pad;
+  /* the same lr / betas in double, as torch.optim.Adam holds them (Python floats): 1 - beta
+     and the bias corrections are formed from these as torch forms them (ABI 9); 0 = use the
+     float fields */
+  double lr_d, beta1_d, beta2_d;
 } swarm_adam_cfg;
 
 /* Learner state for the fused training tick.  Weights/moments are ping-ponged so
