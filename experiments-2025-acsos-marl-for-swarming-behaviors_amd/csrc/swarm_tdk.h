@@ -29,6 +29,14 @@ namespace swarm {
 // node index as K, spread over the waves, each writing its slice of the slab.
 constexpr int kTdRows = 32;
 
+// temporary A/B knobs (tools/ab_build.py only)
+#ifndef SWARM_AB_B2
+#define SWARM_AB_B2 1     // 1: B2 products as 16x16x4 tiles; 0: 32x32x2 node sums
+#endif
+#ifndef SWARM_AB_TREE
+#define SWARM_AB_TREE 1   // 1: pairwise vector sums; 0: sequential
+#endif
+
 // pairwise (tree) sum of K values: each term passes log2(K) roundings instead of up to K - 1 in a
 // sequential sum.  The parameter-gradient elements are sums whose terms cancel, so their fp32
 // error scales with the roundings each term passes (tests/test_gpu_parity_large.py bounds it
@@ -36,6 +44,12 @@ constexpr int kTdRows = 32;
 template <int K>
 __device__ inline float tree_sum(float (&v)[K]) {
   static_assert((K & (K - 1)) == 0, "power of two");
+  if (!SWARM_AB_TREE) {
+    float a = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) a = a + v[i];
+    return a;
+  }
 #pragma unroll
   for (int w = K / 2; w >= 1; w /= 2)
 #pragma unroll
@@ -598,6 +612,29 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
     }
   };
+  auto b2_old = [&](int job) {   // A/B: the 32x32x2 node-sum products (job 0 dW1, job 1 dW2)
+    const int col = lane & 31, h = lane >> 5;
+    float a[16], b[16];
+    int an[16];
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int n = 2 * s2 + h;
+      if (job == 0) { a[s2] = TB.dZ[n][col]; b[s2] = TB.T[n][col]; }
+      else { an[s2] = TB.act[n]; a[s2] = TB.gq[n]; b[s2] = TB.R[n][col]; }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) asm volatile("" : "+v"(a[s2]), "+v"(b[s2]));
+    f32x16 acc = {};
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(job == 0 ? a[s2] : (an[s2] == col ? a[s2] : 0.0f), b[s2], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (job == 0) sst(OFF_W1 + row * kHidden + col, acc[r]);
+      else if (row < kActions) sst(OFF_W2 + row * kHidden + col, acc[r]);
+    }
+  };
   auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
     if (job == 2) {
       if (lane < kHidden) {
@@ -774,7 +811,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
     //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
     //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
-    for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
+    if (SWARM_AB_B2) {
+      for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
+    } else {
+      for (int job = wi; job < 2; job += GPB) b2_old(job);
+    }
     if (np_pre == 0)
       for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
   }

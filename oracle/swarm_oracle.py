@@ -643,6 +643,32 @@ def gcn_conv_dense(params: dict, x: torch.Tensor, mult: torch.Tensor):
     return F.linear(z, params["lin2.weight"], params["lin2.bias"])
 
 
+def gcn_conv_edges(params: dict, x: torch.Tensor, edge_index: torch.Tensor, n_nodes: int) -> torch.Tensor:
+    """a13 in PyG's own edge-list arithmetic (GCNConv 2.5.3, parity unpinned): gcn_norm with
+    add_remaining_self_loops (every self loop dropped, one weight-1 loop per node appended),
+    deg = scatter_add of the edge weights on the target, norm = deg^-1/2[src] * w * deg^-1/2[dst],
+    then out = scatter_add over edges of norm * h[src] + bias, tanh, lin1, relu, lin2.  The same
+    math as gcn_conv_dense, each term formed and summed in a different order: a second fp32
+    evaluation of the gradient (tests/test_gpu_parity_large.py).  x [M, 7], edge_index [2, E]."""
+    W = params["conv1.lin.weight"]
+    h = F.linear(x, W)
+    src, dst = edge_index[0], edge_index[1]
+    keep = src != dst
+    loops = torch.arange(n_nodes)
+    src = torch.cat([src[keep], loops])
+    dst = torch.cat([dst[keep], loops])
+    w = torch.ones(src.shape[0], dtype=h.dtype)
+    deg = torch.zeros(n_nodes, dtype=h.dtype).scatter_add_(0, dst, w)
+    dis = deg.pow(-0.5)
+    dis = torch.where(torch.isinf(dis), torch.zeros_like(dis), dis)
+    norm = dis[src] * w * dis[dst]
+    out = torch.zeros(n_nodes, h.shape[1], dtype=h.dtype).index_add_(0, dst, norm[:, None] * h[src])
+    out = out + params["conv1.bias"]
+    t = torch.tanh(out)
+    z = torch.relu(F.linear(t, params["lin1.weight"], params["lin1.bias"]))
+    return F.linear(z, params["lin2.weight"], params["lin2.bias"])
+
+
 def argmax_first(q: torch.Tensor) -> torch.Tensor:
     """torch.argmax semantics (first maximal index)."""
     return torch.argmax(q, dim=-1)
@@ -771,13 +797,20 @@ def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_sta
     """TD loss and its gradient (train_gcn_dqn.py:113-124) on S sampled graphs of N nodes.
 
     s_state / s_next_state: [S,N,4] (pos, vel); actions [S,N] int; rewards [S,N].
-    conv="gcn": the a13 GCNConv variant (parity unpinned) on complete graphs.
+    conv="gcn": the a13 GCNConv variant (parity unpinned) on complete graphs, in dense form;
+    conv="gcn_edges": the same in PyG's edge-list arithmetic (gcn_conv_edges); conv="gat_dense":
+    the GAT in its dense multiplicity form (q_forward_dense) on complete graphs.  The alternate
+    forms are the same math with every term formed and summed differently: further fp32
+    evaluations for the tests' noise estimates.
     dtype=torch.float64 evaluates the same restatement in double precision from the same fp32
     inputs: the "exact" value both fp32 paths (this oracle and the GPU) are measured against.
     Returns (loss, flat grad [N_PARAMS], online Q at the taken actions, TD targets).
     """
-    if conv == "gcn":
-        return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma, dtype)
+    if conv in ("gcn", "gcn_edges"):
+        return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma, dtype,
+                                 edges=conv == "gcn_edges")
+    if conv == "gat_dense":   # GCN.forward on the dense multiplicity form (q_forward_dense), complete graphs
+        return _td_loss_grad_gat_dense(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma, dtype)
     S, N, _ = s_state.shape
     params = {k: v.to(dtype).clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
     tparams = {k: v.to(dtype) for k, v in unflatten_params(flat_target).items()}
@@ -797,8 +830,8 @@ def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_sta
     return float(loss.item()), grad, values.detach().squeeze(1), target
 
 
-def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma,
-                      dtype=torch.float32):
+def _td_loss_grad_gat_dense(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma,
+                            dtype=torch.float32):
     S, N, _ = s_state.shape
     params = {k: v.to(dtype).clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
     tparams = {k: v.to(dtype) for k, v in unflatten_params(flat_target).items()}
@@ -807,9 +840,34 @@ def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_nex
     xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4]).to(dtype)
     a = actions.reshape(-1).to(torch.long)
     r = rewards.reshape(-1).to(torch.float32).to(dtype)
-    values = gcn_conv_dense(params, x, mult).reshape(S * N, -1).gather(1, a.unsqueeze(1))
+    values = q_forward_dense(params, x, mult).reshape(S * N, -1).gather(1, a.unsqueeze(1))
     with torch.no_grad():
-        next_values = gcn_conv_dense(tparams, xn, mult).reshape(S * N, -1).max(dim=1)[0]
+        next_values = q_forward_dense(tparams, xn, mult).reshape(S * N, -1).max(dim=1)[0]
+    target = r + gamma * next_values
+    loss = torch.nn.MSELoss()(values, target.unsqueeze(1))
+    loss.backward()
+    grad = torch.cat([params[k].grad.reshape(-1) for k, _ in PARAM_ORDER]).clone()
+    return float(loss.item()), grad, values.detach().squeeze(1), target
+
+
+def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma,
+                      dtype=torch.float32, edges: bool = False):
+    S, N, _ = s_state.shape
+    params = {k: v.to(dtype).clone().requires_grad_(True) for k, v in unflatten_params(flat_params).items()}
+    tparams = {k: v.to(dtype) for k, v in unflatten_params(flat_target).items()}
+    mult = multiplicity_complete(S, N).to(dtype)
+    x = node_features(s_state[..., :2], s_state[..., 2:4]).to(dtype)
+    xn = node_features(s_next_state[..., :2], s_next_state[..., 2:4]).to(dtype)
+    a = actions.reshape(-1).to(torch.long)
+    r = rewards.reshape(-1).to(torch.float32).to(dtype)
+    if edges:   # PyG's edge-list arithmetic on the Batch of complete graphs
+        ei = complete_batch_edge_index(S, N)
+        fwd = lambda p_, x_: gcn_conv_edges(p_, x_.reshape(S * N, -1), ei, S * N)  # noqa: E731
+    else:
+        fwd = lambda p_, x_: gcn_conv_dense(p_, x_, mult).reshape(S * N, -1)  # noqa: E731
+    values = fwd(params, x).gather(1, a.unsqueeze(1))
+    with torch.no_grad():
+        next_values = fwd(tparams, xn).max(dim=1)[0]
     target = r + gamma * next_values
     loss = torch.nn.MSELoss()(values, target.unsqueeze(1))
     loss.backward()

@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4: GPU tests of the in-tree library (TESTS="..." selects; default the fused / TD parity set),
-# then an interleaved A/B of the headline bench (and C3) against ab/libswarm_$OLD.so
+# then an interleaved A/B of the headline bench (and C3 with AB_C3=1) over VARIANTS ("base" = the
+# in-tree library, NAME = ab/libswarm_NAME.so)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TESTS=${TESTS:-"tests/test_gpu_parity_act_large.py tests/test_gpu_parity_large.py tests/test_compat_dropin.py tests/test_gpu_parity.py::test_closed_loop_rollout_reproduces_recorded_episodes tests/test_gpu_parity.py::test_td_update_parity tests/test_gpu_parity.py::test_seed_set_after_construction_reaches_the_fused_tick tests/test_gpu_parity.py::test_fused_tick_equals_unfused tests/test_gpu_parity.py::test_one_launch_tick_equals_three_launch_tick"}
@@ -10,11 +11,11 @@ rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|Error" gpurun_out/pytest_new
 cp gpurun_out/parity_errors.gpu.json gpurun_out/parity_errors_new.json 2>/dev/null
 if [ $rc -ne 0 ]; then grep -E "^E |FAILED|assert" gpurun_out/pytest_new.log | head -30; exit $rc; fi
 fi
-OLD=${OLD:-r4v1}
+VARIANTS=${VARIANTS:-"base r4v1"}
 : > gpurun_out/ab.jsonl
 for args in "" ${AB_C3:+"--scenario ObstacleAvoidance --agents 12"}; do
 for rep in 1 2 3; do
-  for v in base $OLD; do
+  for v in $VARIANTS; do
     if [ "$v" = base ]; then lib=""; else lib="$PWD/ab/libswarm_$v.so"; fi
     SWARM_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu-baseline $args > gpurun_out/ab_$v.log 2>&1
     rc=$?
