@@ -490,7 +490,7 @@ def test_td_update_parity(sw, golden_weights, scen, N, S, graph, k, conv):
     elif graph == "radius":
         edge_fn = lambda ss: torch.cat([O.radius_edge_index(ss[g, :, :2], 0.5) + g * N for g in range(ss.shape[0])], dim=1)  # noqa: E731
     _, g32s, _, g64 = oracle_grad_orders(p, tgt, s, a, r, s1, conv=conv, seed=S, edge_fn=edge_fn)
-    _grad_bound_check(f"{scen} N={N} S={S} {graph} {conv}", grad[:O.N_PARAMS], g32s, g64, elementwise=conv == "gat")
+    _grad_bound_check(f"{scen} N={N} S={S} {graph} {conv}", grad[:O.N_PARAMS], g32s, g64)
     eng.adam()
     torch.cuda.synchronize()
     c = eng.read_ctrl()

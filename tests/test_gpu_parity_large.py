@@ -20,12 +20,13 @@ parity_errors.gpu.json via conftest.record and are kept under profiles/):
 - the fp32 oracle's own error: the largest distance to float64 of four fp32 evaluations of the
   same sum (the batch in three orders, and the other formulation: GAT dense / GCN edge-list);
 - gradient, per element: within 1e-4 of the element's magnitude plus 2e-6 of the tensor's largest
-  element (the pre-round-3 bound, restored; round 3 had doubled it to admit a summation-order
-  change), asserted for the reference's network (GAT).  For the a13 GCNConv variant (not in the
-  reference, parity unpinned) it is recorded, not asserted: at C5's 12-agent shard its TD errors
-  are small against Q (delta = Q - y cancels ~two orders of magnitude), so every fp32 evaluation's
-  gradient error is set by Q's last bits, and the fp32 oracle itself reaches 0.5-0.7 of the bound
-  there (on this container's CPU; profiles/r04_parity_errors.json records the GPU's);
+  element (the pre-round-3 bound; round 3 had doubled it to admit a summation-order change, and
+  that doubling is withdrawn) plus 4x the fp32 oracle's own distance to float64 on that very
+  element (largest over the four evaluations).  The last term matters only where the TD error
+  delta = Q - y cancels most of Q (small gradients: C5's first fused tick, the a13 variant at
+  12 agents): there every fp32 evaluation's gradient error is set by Q's last bits, and the fp32
+  oracle itself exceeds the pre-round-3 bound (3.6x on conv1.lin.weight at C5's first fused
+  tick); both ratios are recorded;
 - Adam, isolated from the gradient: m, v and the weights against torch.optim.Adam applied to the
   GPU's OWN gradient: m within 8 ulps and v within 16 ulps of the magnitude of their update terms
   (beta * old + (1 - beta) * new), the weights within 4 ulps of max(|w|, lr);
@@ -109,7 +110,7 @@ def oracle_grad_orders(p, t, s, a, r, s1, conv="gat", seed=0, edge_fn=None):
     return loss32, g32s, loss64, g64
 
 
-def _grad_bound_check(name, g_gpu, g32s, g64, elementwise=True):
+def _grad_bound_check(name, g_gpu, g32s, g64):
     """Gradient vs the float64 evaluation (module docstring).  Gradient elements are sums over S*N
     nodes whose terms cancel, so an element's rounding error scales with its terms, not with its
     value: both fp32 paths sit thousands of ulps of the value away on such elements, and an ulp
@@ -135,26 +136,24 @@ def _grad_bound_check(name, g_gpu, g32s, g64, elementwise=True):
         record(f"{name} grad[{k}] oracle32 vs fp64", st_o32, floor=floor)
         assert st_gpu["max_abs"] <= bound, (name, k, st_gpu["max_abs"], o32_max)
         worst_ratio_t = max(worst_ratio_t, st_gpu["max_abs"] / max(o32_max, 1e-30))
-        # per element: the pre-round-3 bound, 1e-4 of the element's own magnitude plus 2e-6 of the
-        # tensor's largest (the round-3 doubling is withdrawn)
-        elem_bound = 1e-4 * b.abs() + floor
-        ratio = float(((a - b).abs() / elem_bound).max())
-        # diagnostic only (not asserted): the GPU's error against the fp32 oracle's own per-element
-        # noise over its summation orders (the terms themselves are identical in every order, so
-        # this underestimates the noise of an evaluation that also computes the terms differently)
+        # per element: the pre-round-3 bound (1e-4 of the element's magnitude + 2e-6 of the
+        # tensor's largest) plus 4x the fp32 oracle's own distance to float64 on that element
+        # (largest over the four fp32 evaluations): where the TD error cancels most of Q the fp32
+        # oracle itself exceeds the pre-round-3 bound (up to 3.6x at C5's first fused tick)
         noise = torch.stack([(c - b).abs() for c in cs]).max(dim=0).values
-        noise = torch.maximum(noise, noise.median())
+        old = 1e-4 * b.abs() + floor
+        elem_bound = old + 4.0 * noise
+        ratio = float(((a - b).abs() / elem_bound).max())
         record(f"{name} grad[{k}] elementwise: largest error / bound", {
-            "gpu": ratio, "oracle32": float(((cs[0] - b).abs() / elem_bound).max()),
-            "gpu_over_oracle_order_noise": float(((a - b).abs() / (4.0 * noise + 2.0 * fp32_ulp(b))).max())})
+            "gpu": ratio, "gpu_over_pre_r3_bound": float(((a - b).abs() / old).max()),
+            "oracle32_over_pre_r3_bound": float(((cs[0] - b).abs() / old).max())})
         if ratio > worst_elem:
             worst_elem, worst_k = ratio, k
         o += n
     record(f"{name} grad: worst per-tensor ratio gpu/oracle32 error", {"ratio": worst_ratio_t,
                                                                        "worst_elementwise_ratio": worst_elem})
-    if elementwise:
-        assert worst_elem <= 1.0, (f"{name}: a {worst_k} gradient element outside 1e-4 rel + 2e-6 x tensor max "
-                                   f"(ratio {worst_elem:.3f})")
+    assert worst_elem <= 1.0, (f"{name}: a {worst_k} gradient element outside 1e-4 rel + 2e-6 x tensor max + "
+                               f"4x the fp32 oracle's own error on it (ratio {worst_elem:.3f})")
 
 
 def _adam_check(name, p_gpu, m_gpu, v_gpu, p0, g_gpu, m0, v0, step0, norm_gpu=None, lr=1e-3, b1=0.9, b2=0.999):
@@ -195,7 +194,7 @@ def _compare_update(name, eng, p0, t0, idx, S, N, scen, conv):
     record(f"{name} TD loss gpu vs fp64", st_gpu)
     record(f"{name} TD loss oracle32 vs fp64", st_o32)
     assert st_gpu["max_ulp"] <= 4.0 * st_o32["max_ulp"] + 8.0, (st_gpu, st_o32)
-    _grad_bound_check(name, grad[:O.N_PARAMS], g32s, g64, elementwise=conv == "gat")
+    _grad_bound_check(name, grad[:O.N_PARAMS], g32s, g64)
     return g32s[0], grad[:O.N_PARAMS].clone()
 
 
