@@ -69,7 +69,7 @@ class SwarmPeer(ctypes.Structure):
 # swarm_ctrl is 16 x 4-byte words on the device; field -> word index
 CTRL_WORDS = 32
 CTRL = dict(tick=0, write_slot=1, filled_slots=2, adam_step=3, eps=4, loss=5, grad_norm=6, trained=7, episode=8,
-            adam_step_size=14, adam_inv_bc2=15, peer_hold=23)
+            adam_step_size=14, adam_inv_bc2=15, peer_hold=23, one_m_beta1=24, one_m_beta2=25)
 
 _PROTOS = {
     "swarm_abi_version": (c_int32, []),

@@ -187,7 +187,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;
     float gn = 0.0f;
     SWARM_STAMP(20);
-    if (pending) gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, tid, red);
+    if (pending) gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, cc.one_m_beta1, cc.one_m_beta2, tid, red);
     store_w_lds(Pw, R, tid);
     SWARM_STAMP(24);
     if (vb == 0) {

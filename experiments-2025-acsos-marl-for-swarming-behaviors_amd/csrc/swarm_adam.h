@@ -119,8 +119,10 @@ __device__ inline void adam_elem(float g, float& w, float& m, float& v, float on
 // __syncthreads).  step_size / inv_bc2_sqrt: ctrl's scalars of this step.  Returns the
 // pre-clip global norm.  red: LDS scratch of >= kAdamNT/64 floats.
 template <int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
+// one_m_b1 / one_m_b2: ctrl's (float)(1 - beta) (swarm_ctrl_init, from the double betas): read
+// with the control block the prologue loads anyway, not from a kernarg double on its chain
 __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float step_size, float inv_bc2_sqrt,
-                                   int tid, float* red) {
+                                   float one_m_b1, float one_m_b2, int tid, float* red) {
 #define AD_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
   const float inv_w = 1.0f / (float)hp.world_size;
   // clip_grad_norm_: the norm of the per-tensor norms == the global L2 norm up to rounding
@@ -155,8 +157,6 @@ __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float 
   const float coef = hp.max_norm * __builtin_amdgcn_rcpf(total_norm + 1e-6f);
   const float clamped = coef < 1.0f ? coef : 1.0f;
   const float bc2_sqrt = inv_bc2_sqrt;   // reciprocal of sqrt(bias_correction2)
-  const float one_m_b1 = (float)(1.0 - adam_beta1(hp));
-  const float one_m_b2 = (float)(1.0 - adam_beta2(hp));
 #pragma unroll
   for (int j = 0; j < kAdamNJ; ++j) {
     float4 g = R.g[j], w = R.w[j], m = R.m[j], v = R.v[j];

@@ -232,8 +232,6 @@ __device__ inline void pair_force(float dx, float dy, float& fx, float& fy) {
   fy = kCollisionForce * dy / den * pen;
 }
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));   // A/B only
-
 // discrete action a in 0..8 -> u = (L[a/3], L[a%3]), L = {0, -1, +1}  
 __host__ __device__ inline float action_level(int l) { return l == 0 ? 0.0f : (l == 1 ? -1.0f : 1.0f); }
 

@@ -41,9 +41,9 @@ struct ReduceArgs {
 
 // 1024 threads = 16 columns x 64 slab groups (105 column blocks: the 1.7 MB of freshly
 // written slabs is read by many CUs at once, 16 KB each); group g sums a contiguous run of
-// slabs with every load issued before the adds, then the 64 group sums of a column are added
-// in a fixed two-level order (8 runs of 8, then the 8 run sums), every level a pairwise tree
-// (tree_sum, swarm_tdk.h): bitwise reproducible run to run.  Advance mode adds one control block (the last): it prepares
+// slabs with every load issued before the ordered adds, then the 64 group sums of a column
+// are added in a fixed two-level order (8 runs of 8, then the 8 run sums): bitwise
+// reproducible run to run.  Advance mode adds one control block (the last): it prepares
 // and stores the whole ctrl update (Adam scalars of the next step in double, the next
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
 // Three more blocks copy w / m / v _nxt -> _cur (one array each), beside the column blocks.
@@ -151,13 +151,16 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
     v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[slab_index(col, b0 + j, n_slabs)] : 0.0f;
-  float s = tree_sum(v0);
+  float s = v0[0];
+#pragma unroll
+  for (int j = 1; j < kChunk; ++j) s = s + v0[j];
   if (col <= N_PARAMS) {
     for (int b = b0 + kChunk; b < b1; b += kChunk) {
       float v[kChunk];
 #pragma unroll
       for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? slabs[slab_index(col, b + j, n_slabs)] : 0.0f;
-      s = s + tree_sum(v);
+#pragma unroll
+      for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }
   }
   SWARM_STAMP(29);
@@ -165,17 +168,16 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   __syncthreads();
   SWARM_STAMP(30);
   if (q < kRedRuns) {
-    float r[8];
+    float r = part[8 * q][c];
 #pragma unroll
-    for (int gi = 0; gi < 8; ++gi) r[gi] = part[8 * q + gi][c];
-    part2[q][c] = tree_sum(r);
+    for (int gi = 1; gi < 8; ++gi) r = r + part[8 * q + gi][c];
+    part2[q][c] = r;
   }
   __syncthreads();
   if (q == 0 && col <= N_PARAMS) {
-    float t8[kRedRuns];
+    float tot = part2[0][c];
 #pragma unroll
-    for (int gi = 0; gi < kRedRuns; ++gi) t8[gi] = part2[gi][c];
-    const float tot = tree_sum(t8);
+    for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
     if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
     else A.grad[col] = tot;
     // this rank's loss of the update (0 when skipped: the TD launch wrote zero slabs)
@@ -221,6 +223,7 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
   const uint32_t tick = C->tick;
   const uint32_t step = C->adam_step + 1;
   const float step_size = C->adam_step_size, inv_bc2 = C->adam_inv_bc2;
+  const float one_m_b1 = C->one_m_beta1, one_m_b2 = C->one_m_beta2;
   const bool train = A.flush ? (C->trained != 0u && C->peer_hold == 0u)
                              : (valid_slots * (uint32_t)A.B >= (uint32_t)A.hp.batch);
   // target sync: unfused = after the TD step of tick `tick` ((tick+1) % every); flush = the
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
   __syncthreads();   // every thread has read ctrl before thread 0 rewrites it
   float gn = 0.0f;
   if (train) {
-    gn = adam_apply(R, A.hp, step_size, inv_bc2, tid, red);
+    gn = adam_apply(R, A.hp, step_size, inv_bc2, one_m_b1, one_m_b2, tid, red);
     store4(A.params, R.w, R.wt, tid);
     store4(A.m, R.m, R.mt, tid);
     store4(A.v, R.v, R.vt, tid);
@@ -261,6 +264,8 @@ __global__ void ctrl_init_kernel(swarm_adam_cfg hp, float eps, swarm_ctrl* C) {
   for (int i = 0; i < (int)(sizeof(swarm_ctrl) / 4); ++i) w[i] = 0u;
   C->eps = eps;
   C->sample_tick = 0xFFFFFFFFu;   // empty sampling-key cache
+  C->one_m_beta1 = (float)(1.0 - adam_beta1(hp));   // torch: 1 - beta of Python floats
+  C->one_m_beta2 = (float)(1.0 - adam_beta2(hp));
   ctrl_set_double(C, CTRL_B1POW, 1.0);
   ctrl_set_double(C, CTRL_B2POW, 1.0);
   ctrl_store_next_scalars(C, hp);

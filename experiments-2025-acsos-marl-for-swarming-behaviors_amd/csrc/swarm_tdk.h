@@ -29,34 +29,6 @@ namespace swarm {
 // node index as K, spread over the waves, each writing its slice of the slab.
 constexpr int kTdRows = 32;
 
-// temporary A/B knobs (tools/ab_build.py only)
-#ifndef SWARM_AB_B2
-#define SWARM_AB_B2 1     // 1: B2 products as 16x16x4 tiles; 0: 32x32x2 node sums
-#endif
-#ifndef SWARM_AB_TREE
-#define SWARM_AB_TREE 1   // 1: pairwise vector sums; 0: sequential
-#endif
-
-// pairwise (tree) sum of K values: each term passes log2(K) roundings instead of up to K - 1 in a
-// sequential sum.  The parameter-gradient elements are sums whose terms cancel, so their fp32
-// error scales with the roundings each term passes (tests/test_gpu_parity_large.py bounds it
-// against the fp32 oracle's own noise per element)
-template <int K>
-__device__ inline float tree_sum(float (&v)[K]) {
-  static_assert((K & (K - 1)) == 0, "power of two");
-  if (!SWARM_AB_TREE) {
-    float a = v[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i) a = a + v[i];
-    return a;
-  }
-#pragma unroll
-  for (int w = K / 2; w >= 1; w /= 2)
-#pragma unroll
-    for (int i = 0; i < w; ++i) v[i] = v[2 * i] + v[2 * i + 1];
-  return v[0];
-}
-
 template <int NS>
 struct TdLds {
   static constexpr int GPB = kTdRows / NS;
@@ -308,7 +280,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   if (FUSED) {   // the pending optimizer step (train_gcn_dqn.py:125-133), as every acting block does;
                  // done before any hand-off wait so that none of it follows the wait
     const bool pending = cc.trained != 0u && cc.peer_hold == 0u;   // a held rank applies no step
-    if (pending) adam_apply(R, hp, cc.adam_step_size, cc.adam_inv_bc2, threadIdx.x, L.red);
+    if (pending) adam_apply(R, hp, cc.adam_step_size, cc.adam_inv_bc2, cc.one_m_beta1, cc.one_m_beta2, threadIdx.x, L.red);
     store_w_lds(Pon, R, threadIdx.x);
     if (pending && (cc.tick % (uint32_t)hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
     else ptg.store(Ptg, threadIdx.x);
@@ -612,50 +584,35 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
     }
   };
-  auto b2_old = [&](int job) {   // A/B: the 32x32x2 node-sum products (job 0 dW1, job 1 dW2)
-    const int col = lane & 31, h = lane >> 5;
-    float a[16], b[16];
-    int an[16];
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) {
-      const int n = 2 * s2 + h;
-      if (job == 0) { a[s2] = TB.dZ[n][col]; b[s2] = TB.T[n][col]; }
-      else { an[s2] = TB.act[n]; a[s2] = TB.gq[n]; b[s2] = TB.R[n][col]; }
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) asm volatile("" : "+v"(a[s2]), "+v"(b[s2]));
-    f32x16 acc = {};
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(job == 0 ? a[s2] : (an[s2] == col ? a[s2] : 0.0f), b[s2], acc, 0, 0, 0);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (job == 0) sst(OFF_W1 + row * kHidden + col, acc[r]);
-      else if (row < kActions) sst(OFF_W2 + row * kHidden + col, acc[r]);
-    }
-  };
   auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
     if (job == 2) {
       if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
-        sst(OFF_B1 + lane, tree_sum(v));
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        sst(OFF_B1 + lane, acc);
       }
-    } else if (lane < kActions || lane == 63) {   // db2 / loss: the tree sum over the 32 rows (every
-      // read unconditional: as selects around the reads they became a branch and an LDS round
-      // trip per row)
-      int an[kTdRows];
-      float gn[kTdRows], dn[kTdRows];
+    } else if (lane < kActions || lane == 63) {   // db2 / loss: the ordered sum over the 32 rows,
+      // 8 rows' reads at a time (each read unconditional: as selects around the reads they became
+      // a branch and an LDS round trip per row)
+      float acc = 0.0f;
 #pragma unroll
-      for (int n = 0; n < kTdRows; ++n) { an[n] = TB.act[n]; gn[n] = TB.gq[n]; dn[n] = TB.d2[n]; }
+      for (int k = 0; k < kTdRows; k += 8) {
+        int a8[8];
+        float g8[8], d8[8];
 #pragma unroll
-      for (int n = 0; n < kTdRows; ++n) asm volatile("" : "+v"(gn[n]), "+v"(dn[n]));
-      float v[kTdRows];
+        for (int j = 0; j < 8; ++j) { a8[j] = TB.act[k + j]; g8[j] = TB.gq[k + j]; d8[j] = TB.d2[k + j]; }
 #pragma unroll
-      for (int n = 0; n < kTdRows; ++n) v[n] = lane == 63 ? dn[n] : (an[n] == lane ? gn[n] : 0.0f);
-      const float acc = tree_sum(v);
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(g8[j]), "+v"(d8[j]));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = lane == 63 ? d8[j] : (a8[j] == lane ? g8[j] : 0.0f);
+          acc = (k == 0 && j == 0) ? v : acc + v;
+        }
+      }
       sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
     }
   };
@@ -811,11 +768,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
     //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
     //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
-    if (SWARM_AB_B2) {
-      for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
-    } else {
-      for (int job = wi; job < 2; job += GPB) b2_old(job);
-    }
+    for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
     if (np_pre == 0)
       for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
   }
@@ -855,12 +808,18 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
-        sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, tree_sum(v));
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, acc);
       } else if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
         for (int n = 0; n < kTdRows; ++n) v[n] = TB.dO[n][lane];
-        sst(OFF_BIAS + lane, tree_sum(v));
+        float acc = v[0];
+#pragma unroll
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
+        sst(OFF_BIAS + lane, acc);
       }
     }
   }

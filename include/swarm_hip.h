@@ -90,7 +90,9 @@ typedef struct swarm_ctrl {
                              expired on this rank; every later optimizer step is then skipped (the
                              summed gradient is wrong), so a timeout never reaches the weights.
                              Cleared only by swarm_ctrl_init; PeerExchange.check() raises on it. */
-  uint32_t pad1[8];
+  float one_m_beta1;      /* words 24-25: (float)(1 - beta1), (float)(1 - beta2) formed in double from   */
+  float one_m_beta2;      /* swarm_adam_cfg's double betas by swarm_ctrl_init, as torch forms them   */
+  uint32_t pad1[6];
 } swarm_ctrl;           /* 32 words */
 /* A fresh control block comes from swarm_ctrl_init (all counters 0, beta powers 1). */
 
@@ -129,8 +131,8 @@ typedef struct swarm_adam_cfg {
   int32_t world_size;            /* ranks whose gradients are summed (grad /= W)   */
   int32_t pad;
   /* the same lr / betas in double, as torch.optim.Adam holds them (Python floats): 1 - beta
-     and the bias corrections are formed from these as torch forms them (ABI 9); 0 = use the
-     float fields */
+     (into the control block by swarm_ctrl_init) and the bias corrections are formed from these
+     as torch forms them (ABI 9); 0 = use the float fields */
   double lr_d, beta1_d, beta2_d;
 } swarm_adam_cfg;
 
