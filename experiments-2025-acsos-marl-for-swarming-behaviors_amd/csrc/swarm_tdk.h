@@ -49,7 +49,7 @@ struct TdLds {
     };
     WSmall<NS> tgsm[GPB];         // before B1: the target waves' small scratch
   };
-  float y[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];
+  float yq[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];   // yq: gamma max_a Q_target(s')
   int act[kTdRows];
   int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
   int prew[GPB];                  // online wave w is on the pre path (swarm_tdk.h td_body)
@@ -346,19 +346,19 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   if (!online && !waited) __builtin_amdgcn_s_setprio(2);
   dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, A.radius, conv, nullptr, V, online, F);
   // fused: the rest of this tick's transitions, each as late as its first use: a for the online
-  // waves' pre path, r for the target waves' y (published after the acting wave's reward)
-  if (FUSED && waited) {
+  // waves' pre path here; r (published after the acting wave's reward) by the online waves after
+  // it, in their wait for the target waves' y, so no poll sits between the target forward and B1
+  if (FUSED && waited && online) {
     for (int spin = 0;; ++spin) {
       bool ok = true, okc[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         okc[ct] = true;
         if (ho[ct] && !live_drop[ct]) {
-          const unsigned long long g = ld_granule(ho_at(ct, online ? 9 * N : 8 * N, 1));
+          const unsigned long long g = ld_granule(ho_at(ct, 9 * N, 1));
           okc[ct] = !kHoForceDrop && (uint32_t)(g >> 32) == tag;
           ok = ok && okc[ct];
-          if (online) act[ct] = nv[ct] ? (int)(uint32_t)g : 0;
-          else rew[ct] = __uint_as_float((uint32_t)g);
+          act[ct] = nv[ct] ? (int)(uint32_t)g : 0;
         }
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
@@ -369,7 +369,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (online && p == 0) {
+    if (p == 0) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
         if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = nv[ct] ? act[ct] : 0;
@@ -471,6 +471,28 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
   }
+  if (FUSED && waited && online) {   // r of this tick's transitions (y = r + gamma max Q_tgt after B1)
+    for (int spin = 0;; ++spin) {
+      bool ok = true, okc[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        okc[ct] = true;
+        if (ho[ct] && !live_drop[ct]) {
+          const unsigned long long g = ld_granule(ho_at(ct, 8 * N, 1));
+          okc[ct] = !kHoForceDrop && (uint32_t)(g >> 32) == tag;
+          ok = ok && okc[ct];
+          rew[ct] = __uint_as_float((uint32_t)g);
+        }
+      }
+      if (!__builtin_amdgcn_ballot_w64(!ok)) break;
+      if (kHoForceDrop || spin >= kHoSpinLimit) {   // the graph's rows are dropped (online side)
+        if (lane == 0) atomicAdd(X.ho_err, 1u);
+        drop_overrun<NS, GS>(okc, live_drop, nv, c);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   if (!online && p == 0) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
@@ -478,7 +500,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
       for (int a = 1; a < kActions; ++a) qmax = fmaxf(qmax, F.q[ct][a]);
       if (16 * ct + c < NS) {
-        TB.y[row0 + 16 * ct + c] = nv[ct] ? rew[ct] + A.gamma * qmax : 0.0f;
+        TB.yq[row0 + 16 * ct + c] = nv[ct] ? A.gamma * qmax : 0.0f;   // y = r + this (online waves)
         if (FUSED) TB.tdrop[row0 + 16 * ct + c] = live_drop[ct] ? 1 : 0;
       }
     }
@@ -500,7 +522,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       float qa = F.q[ct][0];
 #pragma unroll
       for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? F.q[ct][a] : qa;
-      const float delta = nv[ct] ? (qa - TB.y[row0 + nn]) : 0.0f;
+      const float delta = nv[ct] ? (qa - (rew[ct] + TB.yq[row0 + nn])) : 0.0f;   // y = r + gamma max Q_tgt(s')
       const float gq = delta * A.grad_scale;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
