@@ -16,7 +16,7 @@ launch that wrote it, so two captured sequences are replayed (after warm ticks, 
 and the four parts are compared with the tick period of a captured 100-tick chain of the same
 library (HIP events).  `--lib=stamps` uses the segment-stamps build instead (much slower).
 
-usage: python tools/tick_split_stamps.py [B N] > out.txt
+usage: python tools/tick_split_stamps.py [B N [GoTo|ObstacleAvoidance [gat|gcn]]] > out.txt
 """
 import ctypes
 import json
@@ -48,12 +48,15 @@ def span(a, first, last):
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    scen = sys.argv[3] if len(sys.argv) > 3 else "GoTo"
+    conv = sys.argv[4] if len(sys.argv) > 4 else "gat"
     _lib.load()
     raw = ctypes.CDLL(_lib.LIB_PATH)
     raw.swarm_dbg_stamps_tick.argtypes = [ctypes.c_void_p]
     raw.swarm_dbg_stamps_td.argtypes = [ctypes.c_void_p]
-    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))["weights_go_to"][0])
-    eng = swarm_amd.SwarmEngine("GoTo", N, B, seed=0, params=w0, batch=B, eps=0.05)
+    key = "weights_go_to" if scen == "GoTo" else "weights_obstacle_avoidance"
+    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[key][0])
+    eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=B, eps=0.05, conv=conv)
     assert eng.fused
     eng.reset()
     for _ in range(100):
@@ -74,7 +77,7 @@ def main():
     g_rt = eng.capture(1, lambda: (eng.launch_tick(), eng.launch_reduce_advance(), eng.launch_tick()))
     g_chain = eng.capture(100, tick)
     stream = torch.cuda.current_stream()
-    res = {"B": B, "N": N, "library": _lib.load().swarm_build_info().decode()}
+    res = {"B": B, "N": N, "scenario": scen, "conv": conv, "library": _lib.load().swarm_build_info().decode()}
     rows, gap_rt = [], []
     for rep in range(5):
         for _ in range(3):

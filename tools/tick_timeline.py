@@ -1,7 +1,9 @@
 """Diagnostic: timeline of ONE fused training tick (swarm_train_tick) from in-kernel
 s_memrealtime stamps (100 MHz, chip-wide) of the stamps build (libswarm_hip_stamps.so):
 when the acting waves end, when the TD waves whose graphs come from the tick's own replay
-slot get their hand-off, when the TD waves end.  Times in us from the first wave's entry."""
+slot get their hand-off, when the TD waves end.  Times in us from the first wave's entry.
+
+usage: python tools/tick_timeline.py [B N [GoTo|ObstacleAvoidance [gat|gcn]]]"""
 import ctypes
 import os
 import sys
@@ -21,7 +23,7 @@ from tools.stamps import ACT, ACT_ORDER, TD, TD_ORDER, report  # noqa: E402
 # waves of hand-off graphs take the pre path (swarm_tdk.h): their s wait follows B0 and leads the
 # forward's first segment, their a wait and gq-free backward (dT, g, dp) come before y
 TD_WAIT = {**TD, 2: "Adam + B0 barrier", 16: "s hand-off wait + " + TD[16],
-           3: "a wait + pre path (dT, g MFMA, dp) + (y)", 5: "dQ/dZ + scaled dO/dp images + B2",
+           3: "a wait + pre path (dT, g MFMA, dp) + r wait + (y)", 5: "dQ/dZ + scaled dO/dp images + B2",
            25: "(pre path: nothing)", 26: "B2 jobs (pre online: vector sums)", 6: "B3 barrier wait"}
 TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 25, 27, 26, 6, 7]
 
@@ -33,8 +35,11 @@ def main():
     raw = ctypes.CDLL(_lib.LIB_PATH)
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))["weights_go_to"][0])
-    eng = swarm_amd.SwarmEngine("GoTo", N, B, seed=0, params=w0, batch=B, eps=0.05)
+    scen = sys.argv[3] if len(sys.argv) > 3 else "GoTo"
+    conv = sys.argv[4] if len(sys.argv) > 4 else "gat"
+    key = "weights_go_to" if scen == "GoTo" else "weights_obstacle_avoidance"
+    w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[key][0])
+    eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=B, eps=0.05, conv=conv)
     eng.reset()
     for _ in range(100):
         eng.act(push=True, full_out=False)
@@ -88,7 +93,7 @@ def main():
             if len(tv):
                 print(f"  target TD waves of hand-off graphs ({len(tv)}):")
                 report(tv.reshape(-1), {**TD, 2: "Adam + B0 barrier", 16: "s' hand-off wait + " + TD[16],
-                                        3: "r wait + (y)", 26: "B2 jobs (dW1 / dW2 MFMA products)",
+                                        3: "(y)", 26: "B2 jobs (dW1 / dW2 MFMA products)",
                                         6: "B3 barrier wait"},
                        len(tv), [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 26, 6, 7])
 
