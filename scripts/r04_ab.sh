@@ -1,7 +1,8 @@
 #!/bin/bash
 # round 4: GPU tests of the in-tree library (TESTS="..." selects; default the fused / TD parity set),
 # then an interleaved A/B of the headline bench (and C3 with AB_C3=1) over VARIANTS ("base" = the
-# in-tree library, NAME = ab/libswarm_NAME.so)
+# in-tree library, NAME = ab/libswarm_NAME.so); CONFIGS="a;b" replaces the bench argument sets
+# (';'-separated, "" = the default C2 line)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TESTS=${TESTS:-"tests/test_gpu_parity_act_large.py tests/test_gpu_parity_large.py tests/test_compat_dropin.py tests/test_gpu_parity.py::test_closed_loop_rollout_reproduces_recorded_episodes tests/test_gpu_parity.py::test_td_update_parity tests/test_gpu_parity.py::test_seed_set_after_construction_reaches_the_fused_tick tests/test_gpu_parity.py::test_fused_tick_equals_unfused tests/test_gpu_parity.py::test_one_launch_tick_equals_three_launch_tick"}
@@ -13,8 +14,12 @@ if [ $rc -ne 0 ]; then grep -E "^E |FAILED|assert" gpurun_out/pytest_new.log | h
 fi
 VARIANTS=${VARIANTS:-"base r4v1"}
 : > gpurun_out/ab.jsonl
-for args in "" ${AB_C3:+"--scenario ObstacleAvoidance --agents 12"}; do
-for rep in 1 2 3; do
+CONFIGS=${CONFIGS:-";${AB_C3:+--scenario ObstacleAvoidance --agents 12}"}
+IFS=';' read -r -a CFGS <<< "$CONFIGS"
+for args in "${CFGS[@]}"; do
+[ -z "$args" ] && [ -n "$SEEN_DEFAULT" ] && continue
+[ -z "$args" ] && SEEN_DEFAULT=1
+for rep in $(seq 1 ${REPS:-3}); do
   for v in $VARIANTS; do
     if [ "$v" = base ]; then lib=""; else lib="$PWD/ab/libswarm_$v.so"; fi
     SWARM_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu-baseline $args > gpurun_out/ab_$v.log 2>&1

@@ -96,6 +96,17 @@ def main():
                                         3: "(y)", 26: "B2 jobs (dW1 / dW2 MFMA products)",
                                         6: "B3 barrier wait"},
                        len(tv), [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 26, 6, 7])
+            # the other online wave of a hand-off block (its graphs come from earlier slots): its
+            # whole backward runs after B1, beside the pre wave's remainder and the target tiles
+            npw = td[blocks_waiting, :2].reshape(-1, 32)
+            npw = npw[npw[:, 10] == 0]
+            if len(npw):
+                print(f"  online TD waves without a hand-off graph, in hand-off blocks ({len(npw)}):")
+                report(npw.reshape(-1), {**TD, 2: "Adam + B0 barrier", 26: "(no B2 jobs)", 6: "B3 barrier wait"},
+                       len(npw), [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 24, 25, 27, 26, 6, 7])
+            print("  B2 -> arrival at B3 (stamps 5 -> 26), median cycles: " + ", ".join(
+                f"{k} {np.median(x[:, 26] - x[:, 5]):.0f}" for k, x in
+                (("pre online", wv), ("other online", npw), ("target", tv)) if len(x)))
 
 
 if __name__ == "__main__":
