@@ -273,40 +273,20 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
         if (valid[ct] && p == 3) st_granule(ho_r + 9 * N + 16 * ct + c, ho_tag, (uint32_t)action[ct]);
     }
     if (it == 0) SWARM_STAMP(5);
-    // ---- env.step (VMAS World.step + scenario reward).  Every unordered agent pair is
-    //      evaluated once, by one lane: item k = u (u - 1) / 2 + n (n < u < N) writes slot
-    //      (n, u) and its mirror (u, n) = 0 - f, since pair_force(-d) == -pair_force(d) bit for
-    //      bit (norm2 is even in d, k dx / den pen odd; 0 - f keeps a +0 slot +0).  ObstacleAvoidance
-    //      appends one item per agent, its obstacle pair, into the diagonal slot (n, n), which
-    //      holds no agent pair.  Then every lane sums its agent's forces in VMAS order: 0 + u,
-    //      obstacle pair, agent pairs in ascending partner index.
-    {
-      const int n_pairs = N * (N - 1) / 2;
-      const int items = n_pairs + (SCEN == SWARM_OBSTACLE_AVOIDANCE ? N : 0);
-      constexpr int kMaxItems = NS * (NS - 1) / 2 + (SCEN == SWARM_OBSTACLE_AVOIDANCE ? NS : 0);
-#pragma unroll 1
-      for (int j = 0; j < (kMaxItems + 63) / 64; ++j) {
-        if (64 * j < items) {   // wave-uniform: a round past the last item is skipped
-          const int k = 64 * j + d.lane;
-          int n = 0, u = 0;
-          if (k < n_pairs) {
-            u = (int)((1.0f + sqrtf(8.0f * (float)k + 1.0f)) * 0.5f);
-            u = (u * (u - 1) / 2 > k) ? u - 1 : u;
-            u = ((u + 1) * u / 2 <= k) ? u + 1 : u;
-            n = k - u * (u - 1) / 2;
-          } else if (k < items) {
-            n = k - n_pairs;
-            u = n;
-          }
-          const bool obst = k >= n_pairs;
-          const float ox = obst ? kObstX : sm.px[u], oy = obst ? kObstY : sm.py[u];
-          float gx = 0.0f, gy = 0.0f;
-          if (k < items) pair_force(sm.px[n] - ox, sm.py[n] - oy, gx, gy);
-          if (k < items) {
-            *reinterpret_cast<float2*>(fb + 2 * (n * NS + u)) = make_float2(gx, gy);
-            if (!obst) *reinterpret_cast<float2*>(fb + 2 * (u * NS + n)) = make_float2(0.0f - gx, 0.0f - gy);
-          }
-        }
+    // ---- env.step (VMAS World.step + scenario reward).  The 4 row groups of an agent
+    //      split its partner pairs (group p: partners p, p + 4, ...), then every lane sums
+    //      the forces in VMAS order: 0 + u, obstacle pair, agent pairs in ascending partner
+    //      index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
+    {   // pair mapping independent of the D layout: 64 / NS lanes per agent (NS = 8: one pair per lane)
+      constexpr int LPN = 64 / NS;
+      const int n = d.lane / LPN;
+      const float pxn = sm.px[n], pyn = sm.py[n];
+#pragma unroll
+      for (int j = 0; j < NS / LPN; ++j) {
+        const int u = d.lane % LPN + LPN * j;
+        float gx = 0.0f, gy = 0.0f;
+        if (u < N && n < N) pair_force(pxn - sm.px[u], pyn - sm.py[u], gx, gy);   // u == n: exactly 0
+        *reinterpret_cast<float2*>(fb + 2 * (n * NS + u)) = make_float2(gx, gy);
       }
     }
     if (it == 0) SWARM_STAMP(6);
@@ -318,22 +298,18 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       const int n = min(16 * ct + c, NS - 1);
       float fx = 0.0f + action_level(action[ct] / 3);
       float fy = 0.0f + action_level(action[ct] % 3);
-      // every slot read at once, no per-partner branch; the slots that hold no agent pair (the
-      // diagonal, partners >= N: not written this tick) add +0, and fx, fy (started from +0 or
-      // +-1) never become -0, so adding +0 is exact
+      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {
+        float gx, gy;
+        pair_force(px[ct] - kObstX, py[ct] - kObstY, gx, gy);
+        fx = fx + gx; fy = fy + gy;
+      }
+      // every slot read at once, no per-partner branch: slots u >= N hold +0 and fx, fy
+      // (started from +0 or +-1) never become -0, so adding them is exact
       float2 f[NS];
 #pragma unroll
       for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + u));
-      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {   // the obstacle pair, from the diagonal slot
-        const float2 fo = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + n));
-        fx = fx + fo.x; fy = fy + fo.y;
-      }
 #pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        const bool pr = u < N && u != n;
-        fx = fx + (pr ? f[u].x : 0.0f);
-        fy = fy + (pr ? f[u].y : 0.0f);
-      }
+      for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
       o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
       if (MODE == MODE_TICK && HO && ho_r && valid[ct]) {
         const int nn = 16 * ct + c;
