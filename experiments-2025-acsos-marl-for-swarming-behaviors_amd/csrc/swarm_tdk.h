@@ -53,6 +53,7 @@ struct TdLds {
   int act[kTdRows];
   int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
   int prew[GPB];                  // online wave w is on the pre path (swarm_tdk.h td_body)
+  int insl[GPB];                  // before B0: online wave w holds a graph of this tick's slot
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
   __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
 };
@@ -269,11 +270,14 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   SWARM_STAMP(1);
   const bool waited = FUSED && __builtin_amdgcn_ballot_w64(wait) != 0;
-  // pre path: the online wave of a graph pair holding one of this tick's transitions forms its
+  // pre path: the online waves of a block holding one of this tick's transitions form their
   // backward for gq = 1 before y (dZ, dT, dO, the attention scores' g and dp are linear in their
   // target node's gq; the sums that mix targets, da_src and dh, stay after B2), in the time the
-  // block waits for the acting wave's s' and the target forward
-  const bool pre = online && __builtin_amdgcn_ballot_w64(inslot) != 0;
+  // block waits for the acting wave's s' and the target forward.  Every online wave of such a
+  // block takes it (round 4): the one without a hand-off graph otherwise ran its whole backward
+  // after B1 and was the last to reach B3.  The rule depends only on the block's graphs, so the
+  // fused, 3-launch and unfused launches still agree bit for bit
+  if (online && lane == 0) TB.insl[wi] = __builtin_amdgcn_ballot_w64(inslot) != 0 ? 1 : 0;
   bool live_drop[CT];   // this wave's graph was dropped after a hand-off overrun
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) live_drop[ct] = false;
@@ -295,6 +299,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   __syncthreads();   // B0: weight images
   SWARM_STAMP(2);
+  bool pre = false;
+#pragma unroll
+  for (int w2 = 0; w2 < GPB; ++w2) pre = pre || TB.insl[w2] != 0;
+  pre = pre && online;
   const uint32_t tag = cc.tick + 1u;
   // granule address of this lane's node in a hand-off record: s at 0, s' at 4N, r at 8N, a at 9N
   auto ho_at = [&](int ct, int off, int per_node) -> const unsigned long long* {
