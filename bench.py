@@ -207,7 +207,8 @@ def main():
     from swarm_amd import dist as swdist
     pg = swdist.init_process_group(args.backend, local_rank) if distributed else None
     from swarm_amd import build as swbuild
-    if rank == 0 and not swbuild.up_to_date():
+    # an explicit SWARM_LIB_PATH (A/B runs of a prebuilt library) is never rebuilt here
+    if rank == 0 and not os.environ.get("SWARM_LIB_PATH") and not swbuild.up_to_date():
         swbuild.build()
     if distributed:
         torch.distributed.barrier()
