@@ -18,7 +18,6 @@
 #pragma once
 #include "swarm_adam.h"
 #include "swarm_dl.h"
-#include <type_traits>
 
 namespace swarm {
 
@@ -28,9 +27,6 @@ namespace swarm {
 // (y = r + gamma max_a Q_tgt), then shares the parameter products.  The parameter
 // gradient of the block is a sum over its 32 node rows: MFMA 16x16x4 f32 tiles with the
 // node index as K, spread over the waves, each writing its slice of the slab.
-#ifndef SWARM_B2_SPLIT   // A/B: hand-off blocks' dW2 tiles on the online waves (tools/ab_build.py)
-#define SWARM_B2_SPLIT 0
-#endif
 constexpr int kTdRows = 32;
 
 template <int NS>
@@ -589,47 +585,33 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // chains interleaved with every operand read first (as conditional reads they became a branch
   // and an LDS round trip in front of each MFMA): 24 MFMAs of 32 cycles where the 32x32x2 form
   // had 16 of 64 per product, and dW2 takes 16 rows of work instead of 32.
-  // W1 / W2 (compile-time): the tile set one wave runs (dW1's two tiles of the column half, dW2's)
-  auto b2_tiles = [&](auto W1, auto W2, int tj) {   // lane (c, p) of the D layout: column c, k-slot / row group p
-    constexpr bool w1 = decltype(W1)::value, w2 = decltype(W2)::value;
+  auto b2_tiles = [&](int tj) {   // lane (c, p) of the D layout: column c, k-slot / row group p
     float a1[2][8], b1[8], a2[8], b2v[8];
     int an[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int n = 4 * s + p;
-      if constexpr (w1) {
-        a1[0][s] = TB.dZ[n][c];
-        a1[1][s] = TB.dZ[n][16 + c];
-        b1[s] = TB.T[n][16 * tj + c];
-      }
-      if constexpr (w2) {
-        b2v[s] = TB.R[n][16 * tj + c];
-        an[s] = TB.act[n];
-        a2[s] = TB.gq[n];
-      }
+      a1[0][s] = TB.dZ[n][c];
+      a1[1][s] = TB.dZ[n][16 + c];
+      b1[s] = TB.T[n][16 * tj + c];
+      b2v[s] = TB.R[n][16 * tj + c];
+      an[s] = TB.act[n];
+      a2[s] = TB.gq[n];
     }
-    if constexpr (w2) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
-    }
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      if constexpr (w1) {
-        d0 = mfma16(a1[0][s], b1[s], d0);
-        d1 = mfma16(a1[1][s], b1[s], d1);
-      }
-      if constexpr (w2) d2 = mfma16(an[s] == c ? a2[s] : 0.0f, b2v[s], d2);
+      d0 = mfma16(a1[0][s], b1[s], d0);
+      d1 = mfma16(a1[1][s], b1[s], d1);
+      d2 = mfma16(an[s] == c ? a2[s] : 0.0f, b2v[s], d2);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if constexpr (w1) {
-        sst(OFF_W1 + (4 * p + r) * kHidden + 16 * tj + c, d0[r]);
-        sst(OFF_W1 + (16 + 4 * p + r) * kHidden + 16 * tj + c, d1[r]);
-      }
-      if constexpr (w2) {
-        if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
-      }
+      sst(OFF_W1 + (4 * p + r) * kHidden + 16 * tj + c, d0[r]);
+      sst(OFF_W1 + (16 + 4 * p + r) * kHidden + 16 * tj + c, d1[r]);
+      if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
     }
   };
   auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
@@ -816,17 +798,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
     //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
     //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
-    if (SWARM_B2_SPLIT && np_pre == GPB) {   // every online wave on the pre path: they take dW2
-      for (int tj = wi; tj < 2; tj += GPB) b2_tiles(std::true_type{}, std::false_type{}, tj);
-    } else {
-      for (int tj = wi; tj < 2; tj += GPB) b2_tiles(std::true_type{}, std::true_type{}, tj);
-    }
+    for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
     if (np_pre == 0)
       for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
   }
   if (online && pre) {   // (GPB = 2: one pre wave takes both sums, two split them)
-    if (SWARM_B2_SPLIT && np_pre == GPB)
-      for (int tj = wi; tj < 2; tj += GPB) b2_tiles(std::false_type{}, std::true_type{}, tj);
     if (np_pre == 1 || wi == 0) b2_job(2);
     if (np_pre == 1 || wi == 1) b2_job(3);
   }
