@@ -40,11 +40,20 @@ def source_digest(extra=()) -> str:
     return h.hexdigest()[:16]
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(OUT):
+def _current(out: str, extra=()) -> bool:
+    """`out` is current: no source newer than it, or (a checkout touched the sources' times)
+    it carries the digest of the sources and flags as they are now."""
+    if not os.path.exists(out):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(f) <= t for f in _deps())
+    t = os.path.getmtime(out)
+    if all(os.path.getmtime(f) <= t for f in _deps()):
+        return True
+    with open(out, "rb") as f:
+        return f"src {source_digest(extra)}".encode() in f.read()
+
+
+def up_to_date() -> bool:
+    return _current(OUT)
 
 
 STAMPS_OUT = os.path.join(HERE, "libswarm_hip_stamps.so")
@@ -64,7 +73,7 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False, varia
     if out is None:
         out, extra = VARIANTS["stamps" if stamps else variant]
     extra = list(extra or [])
-    if not force and os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in _deps()):
+    if not force and _current(out, extra):
         return out
     # one hipcc process per translation unit (in parallel), then one link
     objs = [f"{out}.{os.path.splitext(src)[0]}.o" for src in SOURCES]
