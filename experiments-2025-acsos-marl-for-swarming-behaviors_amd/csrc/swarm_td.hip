@@ -145,12 +145,15 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   const int q = threadIdx.x / kRedCols;
   const int per = (n_slabs + kRedGroups - 1) / kRedGroups;
   const int b0 = q * per, b1 = min(n_slabs, b0 + per);
-  // first chunk of this thread's slab column in flight before anything else
+  // first chunk of this thread's slab column in flight before anything else.  Column col of
+  // slab b is scol[16 b] (swarm_common.h slab_index): one 64-bit base per thread, 32-bit offsets
   constexpr int kChunk = kRedChunk;
+  static_assert(kSlabCols == 16, "slab column blocks of 16");
+  const float* const scol = slabs + ((size_t)(col >> 4) * (size_t)n_slabs * kSlabCols + (size_t)(col & 15));
   float v0[kChunk];
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
-    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? slabs[slab_index(col, b0 + j, n_slabs)] : 0.0f;
+    v0[j] = (col <= N_PARAMS && b0 + j < b1) ? scol[(uint32_t)(b0 + j) * kSlabCols] : 0.0f;
   float s = v0[0];
 #pragma unroll
   for (int j = 1; j < kChunk; ++j) s = s + v0[j];
@@ -158,7 +161,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     for (int b = b0 + kChunk; b < b1; b += kChunk) {
       float v[kChunk];
 #pragma unroll
-      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? slabs[slab_index(col, b + j, n_slabs)] : 0.0f;
+      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? scol[(uint32_t)(b + j) * kSlabCols] : 0.0f;
 #pragma unroll
       for (int j = 0; j < kChunk; ++j) s = s + v[j];
     }

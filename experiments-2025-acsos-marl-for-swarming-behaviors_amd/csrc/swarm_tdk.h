@@ -169,8 +169,13 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   const int row0 = wi * NS;
   const WView<NS> V = online ? WView<NS>{TB.H + row0, TB.T + row0, TB.R + row0, &TB.on[wi]} : TB.target_view(wi);
   const int lane = d.lane, c = d.c, p = d.p;
-  // this block's slab column q (swarm_common.h slab_index: column-block major)
-  auto sst = [&](int q, float v) { slab_st(A.slabs + slab_index(q, vb, A.n_slabs), v); };
+  // this block's slab column q (swarm_common.h slab_index: column-block major), addressed as a
+  // wave-uniform base (the block's 16-column run in column block 0) plus a 32-bit element
+  // offset: one 64-bit add per block instead of 64-bit index arithmetic per store
+  static_assert(kSlabCols == 16, "slab column blocks of 16");
+  float* const slab_base = A.slabs + (size_t)vb * kSlabCols;
+  const uint32_t slab_stride = (uint32_t)A.n_slabs * kSlabCols;
+  auto sst = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
