@@ -311,3 +311,20 @@ def test_engine_refuses_cpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         swarm_amd.SwarmEngine("GoTo", 8, 4)
+
+
+def test_library_is_current_by_source_digest(tmp_path):
+    """build._current: a library whose file time is older than the sources (a checkout touched
+    them) still counts as current when it carries the digest of the sources as they are now;
+    another digest does not."""
+    from swarm_amd import build as b
+    old = min(os.path.getmtime(f) for f in b._deps()) - 100.0
+    good, bad = tmp_path / "good.so", tmp_path / "bad.so"
+    good.write_bytes(b"\x7fELF...libswarm_hip gfx950 abi 9 src " + b.source_digest().encode() + b"\x00")
+    bad.write_bytes(b"\x7fELF...libswarm_hip gfx950 abi 9 src 0123456789abcdef\x00")
+    for f in (good, bad):
+        os.utime(f, (old, old))
+    assert b._current(str(good)) and not b._current(str(bad))
+    assert not b._current(str(tmp_path / "missing.so"))
+    # a variant's digest covers its extra flags
+    assert not b._current(str(good), ["-DSWARM_STAMPS=2"])
