@@ -361,7 +361,7 @@ int swarm_train_act_step(const swarm_config* cfg, const swarm_adam_cfg* hp, cons
     return SWARM_E_BADARG;
   if (cfg->net != SWARM_NET_GCN) return SWARM_E_UNSUPPORTED;   // GAT3: forward only
   ActArgs a = make_args(cfg);
-  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = adam_hp(*hp); a.sample_out = sample_out;
+  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = sample_out;
   a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
   if (replay) a.replay = *replay;
   if (out) a.out = *out;

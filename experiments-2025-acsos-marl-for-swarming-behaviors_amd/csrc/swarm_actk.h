@@ -34,7 +34,7 @@ struct ActArgs {
   float eps;
   int learn;               // MODE_TICK: apply the pending optimizer step first (fused tick)
   swarm_learner lr;
-  AdamHp hp;              // the float / int hyper-parameters (swarm_adam.h adam_hp)
+  swarm_adam_cfg hp;
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
   int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
   unsigned long long* ho_rec;   // fused tick: [B][ho_stride_granules(N)] hand-off records (swarm_common.h)

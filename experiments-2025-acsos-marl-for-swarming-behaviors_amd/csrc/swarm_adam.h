@@ -37,17 +37,6 @@ constexpr int CTRL_B2POW = 2;   // beta_pow[2..3] = beta2^adam_step
 // float field): torch forms 1 - beta1 = 0.1, 1 - beta2 = 0.001 and the bias corrections from
 // Python floats, and (float)(1 - (double)0.999f) is 1.3e-5 away from 0.001f, a systematic
 // 200-ulp bias on v
-// The float / int hyper-parameters an optimizer prologue reads: swarm_adam_cfg without its double
-// fields (ABI 9), so the tick kernels' argument structs stay the size they were in ABI 8 (the
-// doubles are read only where 1 - beta and the bias corrections are formed: swarm_ctrl_init and
-// the reduce's control block)
-struct AdamHp {
-  float lr, beta1, beta2, eps, max_norm, gamma;
-  int32_t batch, update_target_every, world_size, pad;
-};
-__host__ __device__ inline AdamHp adam_hp(const swarm_adam_cfg& c) {
-  return AdamHp{c.lr, c.beta1, c.beta2, c.eps, c.max_norm, c.gamma, c.batch, c.update_target_every, c.world_size, 0};
-}
 __device__ inline double adam_lr(const swarm_adam_cfg& hp) { return hp.lr_d != 0.0 ? hp.lr_d : (double)hp.lr; }
 __device__ inline double adam_beta1(const swarm_adam_cfg& hp) { return hp.beta1_d != 0.0 ? hp.beta1_d : (double)hp.beta1; }
 __device__ inline double adam_beta2(const swarm_adam_cfg& hp) { return hp.beta2_d != 0.0 ? hp.beta2_d : (double)hp.beta2; }
@@ -129,10 +118,10 @@ __device__ inline void adam_elem(float g, float& w, float& m, float& v, float on
 // One optimizer step in registers by the whole workgroup (kAdamNT threads; contains
 // __syncthreads).  step_size / inv_bc2_sqrt: ctrl's scalars of this step.  Returns the
 // pre-clip global norm.  red: LDS scratch of >= kAdamNT/64 floats.
-template <int SB = -1, class HP = AdamHp>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
+template <int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
 // one_m_b1 / one_m_b2: ctrl's (float)(1 - beta) (swarm_ctrl_init, from the double betas): read
 // with the control block the prologue loads anyway, not from a kernarg double on its chain
-__device__ inline float adam_apply(AdamRegs& R, const HP& hp, float step_size, float inv_bc2_sqrt,
+__device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float step_size, float inv_bc2_sqrt,
                                    float one_m_b1, float one_m_b2, int tid, float* red) {
 #define AD_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
   const float inv_w = 1.0f / (float)hp.world_size;

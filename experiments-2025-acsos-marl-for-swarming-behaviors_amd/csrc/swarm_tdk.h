@@ -95,7 +95,7 @@ struct TdSmem {
 // drawn in-kernel, this tick's slot read from the acting waves' hand-off records
 struct TdFused {
   swarm_learner lr;
-  AdamHp hp;                          // the float / int hyper-parameters (swarm_adam.h adam_hp)
+  swarm_adam_cfg hp;
   const unsigned long long* ho_rec;   // [B][ho_stride_granules(N)] tagged hand-off records
   uint32_t* ho_err;                   // bounded-wait overruns (0 in a correct run)
 };
@@ -195,7 +195,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // write_slot, the batch size S, the Adam hyper-parameters) made opaque here, so they are
   // loaded with the first scalar wait instead of being re-fetched at a later first use behind a
   // second one (a kernarg / ctrl round trip on the TD chain)
-  AdamHp hp = X.hp;
+  swarm_adam_cfg hp = X.hp;
   int32_t* sample_out = A.sample_out;
   const unsigned long long* ho_rec = X.ho_rec;
   if (FUSED) {

@@ -91,7 +91,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   a.B = B; a.N = N; a.scenario = cfg->scenario; a.graph = cfg->graph; a.k = cfg->knn_k; a.conv = cfg->conv;
   a.env_offset = cfg->env_offset; a.flags = cfg->flags;
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu); a.k1 = (uint32_t)(cfg->seed >> 32); a.radius = cfg->radius;
-  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = adam_hp(*hp); a.sample_out = nullptr;
+  a.state = state; a.ctrl = ctrl; a.learn = 1; a.lr = *lr; a.hp = *hp; a.sample_out = nullptr;
   a.grad_norm_out = const_cast<float*>(&ctrl->grad_norm);
   a.replay = *replay;
   if (out) a.out = *out;
@@ -106,7 +106,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   t.grad_scale = (float)(2.0 / ((double)hp->batch * (double)N));
 
   TdFused x = {};
-  x.lr = *lr; x.hp = adam_hp(*hp); x.ho_rec = rec; x.ho_err = err;
+  x.lr = *lr; x.hp = *hp; x.ho_rec = rec; x.ho_err = err;
 
   const int n_act = (B + kActWPB - 1) / kActWPB;
   const int gs = N <= 8 ? 8 : 16;
