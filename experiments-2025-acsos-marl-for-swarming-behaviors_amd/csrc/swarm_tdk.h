@@ -54,7 +54,6 @@ struct TdLds {
   int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
   int prew[GPB];                  // online wave w is on the pre path (swarm_tdk.h td_body)
   int insl[GPB];                  // before B0: online wave w holds a graph of this tick's slot
-  int b2cnt;                      // B2 as a count: online waves whose dZ / gq / d2 rows are written
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
   __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
 };
@@ -521,7 +520,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   if (!online && !waited) __builtin_amdgcn_s_setprio(0);
   if (online && lane == 0) TB.prew[wi] = pre ? 1 : 0;
-  if (threadIdx.x == 0) TB.b2cnt = 0;
   SWARM_STAMP(3);
   __syncthreads();   // B1: TD targets
   SWARM_STAMP(4);
@@ -530,7 +528,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   float dz[CT][2][4];
   if (online) {
     // ---- dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ, dZ = dR * [z > 0]
-    float gqs[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c, nn = min(n, NS - 1);
@@ -540,7 +537,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? F.q[ct][a] : qa;
       const float delta = nv[ct] ? (qa - (rew[ct] + TB.yq[row0 + nn])) : 0.0f;   // y = r + gamma max Q_tgt(s')
       const float gq = delta * A.grad_scale;
-      gqs[ct] = gq;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const float4 w = *reinterpret_cast<const float4*>(P + L_W2 + act[ct] * kWRow + 16 * t + 4 * p);
@@ -553,25 +549,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         const int row = row0 + n;
         *reinterpret_cast<float4*>(&TB.dZ[row][4 * p]) = make_float4(dz[ct][0][0], dz[ct][0][1], dz[ct][0][2], dz[ct][0][3]);
         *reinterpret_cast<float4*>(&TB.dZ[row][16 + 4 * p]) = make_float4(dz[ct][1][0], dz[ct][1][1], dz[ct][1][2], dz[ct][1][3]);
-        if (p == 0) { TB.gq[row] = gq; TB.d2[row] = delta * delta; }
-      }
-    }
-    // B2 as a count (round 4): the rows the block's products need (dZ, gq, d2) are written, so
-    // the target waves' tiles and the vector sums may start; this wave's own-row images (X, cm,
-    // the pre path's scaled dO / dp) follow without holding them
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(&TB.b2cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int n = 16 * ct + c;
-      const float gq = gqs[ct];
-      if (n < NS) {
-        const int row = row0 + n;
         TB.X[row][p] = F.x[ct][0];
         TB.X[row][4 + p] = F.x[ct][1];
 #pragma unroll
         for (int j = 0; j < NS / 4; ++j) TB.cm[row][4 * j + p] = pick4(F.cf[ct], j, p);
-        if (p == 0) TB.X[row][8] = 0.0f;
+        if (p == 0) { TB.X[row][8] = 0.0f; TB.gq[row] = gq; TB.d2[row] = delta * delta; }
       }
       if (pre) {   // the pre path's images scaled by this node's gq (rows free since B1)
         float o[2][4];
@@ -595,13 +577,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         dad1[ct] = nv[ct] ? dad1[ct] * gq : 0.0f;
       }
     }
-    wave_lds_sync();   // this wave's own rows (cm, dO, dp) before its dh reads them
   }
-  // the products over all of the block's rows wait for every online wave's count
-  auto wait_b2 = [&]() {
-    while (__hip_atomic_load(&TB.b2cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < GPB)
-      __builtin_amdgcn_s_sleep(1);
-  };
+  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph (pre path: dO / dp too)
   SWARM_STAMP(5);
   int np_pre = 0;   // online waves of this block on the pre path
 #pragma unroll
@@ -826,13 +803,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
     //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
     //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
-    wait_b2();
     for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
     if (np_pre == 0)
       for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
   }
   if (online && pre) {   // (GPB = 2: one pre wave takes both sums, two split them)
-    wait_b2();
     if (np_pre == 1 || wi == 0) b2_job(2);
     if (np_pre == 1 || wi == 1) b2_job(3);
   }
