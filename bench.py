@@ -169,19 +169,27 @@ def spawn_ranks(argv, n: int, script: str = None) -> int:
     or rank 0's JSON line does not report n GPUs."""
     cmd = rank_launch_cmd(argv, n, free_port(), script)
     print("[bench] starting %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    # own session: on any exit of the relay other than its normal end (an exception, ^C, SIGTERM
+    # turned into SystemExit) the whole launcher process group is terminated, ranks included
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)
     line = None
-    for raw in proc.stdout:
-        sys.stdout.write(raw)
-        sys.stdout.flush()
-        if raw.lstrip().startswith("{"):
-            try:
-                d = json.loads(raw)
-            except ValueError:
-                continue
-            if "n_gpus" in d:
-                line = d
-    rc = proc.wait()
+    done = False
+    try:
+        for raw in proc.stdout:
+            sys.stdout.write(raw)
+            sys.stdout.flush()
+            if raw.lstrip().startswith("{"):
+                try:
+                    d = json.loads(raw)
+                except ValueError:
+                    continue
+                if "n_gpus" in d:
+                    line = d
+        rc = proc.wait()
+        done = True
+    finally:
+        if not done:
+            stop_group(proc)
     if rc != 0:
         print(f"[bench] rank launcher exited with {rc}", file=sys.stderr)
         return rc
@@ -190,6 +198,21 @@ def spawn_ranks(argv, n: int, script: str = None) -> int:
               file=sys.stderr)
         return 3
     return 0
+
+
+def stop_group(proc, grace: float = 10.0) -> None:
+    """SIGTERM the launcher's process group (it leads its own session), SIGKILL after `grace` s."""
+    import signal
+    for sig in (signal.SIGTERM, signal.SIGKILL):
+        try:
+            os.killpg(proc.pid, sig)
+        except (ProcessLookupError, PermissionError):
+            return
+        try:
+            proc.wait(timeout=grace)
+            return
+        except subprocess.TimeoutExpired:
+            continue
 
 
 def main():
@@ -457,24 +480,20 @@ def main():
                 "kernel_us": {k: round(v, 2) for k, v in kt.items()}}
 
     # SURVEY §8(d)'s second number: acting-only (S = 0, frozen weights, eps 0, like
-    # Simulator.run_simulation) on the same engine and graph, one swarm_rollout launch per
-    # max_steps-tick episode; after the timed region, one GPU only
+    # Simulator.run_simulation), one swarm_rollout launch per max_steps-tick episode, after the
+    # timed region, one GPU only.  The headline acting line runs the reference's EVALUATION graph,
+    # kNN with k = min(10, N) (simulator.py:19 uses k = 10, which needs N >= 10; at 8 agents the
+    # recorded evaluations ran k = 5, data/test_stats); the training graph (this engine's) is
+    # reported beside it, labelled
     acting = None
     if world == 1:
-        def rollouts(n):
-            for i in range(n):
-                eng.reset()
-                eng.rollout(max_steps, tick0=i * max_steps, eps=0.0)
-        rollouts(3)
-        torch.cuda.synchronize()
-        a0 = time.perf_counter()
-        rollouts(20)
-        torch.cuda.synchronize()
-        a_el = time.perf_counter() - a0
-        acting = {"value": round(B * N * 20 * max_steps / a_el, 1), "unit": "agent-steps/s",
-                  "us_per_tick": round(a_el / (20 * max_steps) * 1e6, 3),
-                  "step": f"reset + {max_steps}-tick rollout launch (swarm_rollout), 20 steps",
-                  "graph": args.graph}
+        import swarm_amd
+        k_eval = min(10, N) if N >= 10 else min(5, N)
+        e_knn = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, graph="knn", knn_k=k_eval, conv=args.conv,
+                                      learn=False, eps=0.0)
+        acting = acting_leg(argparse.Namespace(**{**vars(args), "graph": "knn", "knn_k": k_eval}), e_knn, max_steps)
+        del e_knn
+        acting["training_graph"] = acting_leg(args, eng, max_steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -624,6 +643,61 @@ def cpu_baseline_leg(args, w0, scen, B, N, S, eng):
                                       "sample": "40 episodes, reset + one 50-tick swarm_rollout launch each"}}}
 
 
+def rollout_roofline(args, eng, max_steps, f_node):
+    """The rollout kernel's roofline: algorithmic FLOPs of one max_steps-tick swarm_rollout launch
+    (B·N·ticks·(forward + ≈300 FLOP of physics)) ÷ that launch's duration, HIP events on its stream
+    (median of 5 launches), against the FP32 peak."""
+    B, N = args.envs, args.agents
+    stream = torch.cuda.current_stream()
+    per = []
+    for _ in range(5):
+        eng.reset()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        eng.rollout(max_steps, eps=0.0)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        per.append(e0.elapsed_time(e1) * 1e-3)
+    t_l = float(np.median(per))
+    flops = B * N * max_steps * f_node
+    ach = flops / t_l / 1e12
+    return {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
+            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": None,
+            "kernel": "act_kernel rollout (swarm_rollout)", "algorithmic_flops_per_launch": flops,
+            "flops_per_agent_step": f_node, "launch_us": round(t_l * 1e6, 2)}
+
+
+def acting_fnode(args, eng) -> float:
+    d = mean_in_degree(args, eng)
+    if args.net == "gat3":
+        return gat3_fwd_flops(args.agents, d) + 300
+    return (gat_fwd_flops(args.agents, d) if args.conv == "gat" else gcn_fwd_flops(args.agents, d)) + 300
+
+
+def acting_leg(args, eng, max_steps, n_steps: int = 20) -> dict:
+    """Acting-only rollouts on `eng` (frozen weights, eps 0): n_steps episodes of reset + one
+    max_steps-tick swarm_rollout launch, host wall clock, plus the rollout kernel's roofline."""
+    B, N = args.envs, args.agents
+
+    def rollouts(n):
+        for i in range(n):
+            eng.reset()
+            eng.rollout(max_steps, tick0=i * max_steps, eps=0.0)
+    rollouts(3)
+    torch.cuda.synchronize()
+    a0 = time.perf_counter()
+    rollouts(n_steps)
+    torch.cuda.synchronize()
+    a_el = time.perf_counter() - a0
+    g = {"complete": "complete", "knn": f"kNN-{args.knn_k}", "radius": f"radius-{args.radius}"}[args.graph]
+    out = {"value": round(B * N * n_steps * max_steps / a_el, 1), "unit": "agent-steps/s",
+           "us_per_tick": round(a_el / (n_steps * max_steps) * 1e6, 3),
+           "step": f"reset + {max_steps}-tick rollout launch (swarm_rollout), {n_steps} steps", "graph": g}
+    if not args.no_kernel_timing:
+        out["roofline"] = rollout_roofline(args, eng, max_steps, acting_fnode(args, eng))
+    return out
+
+
 def bench_act(args, eng, world, rank, distributed, max_steps):
     """Acting-only throughput (SURVEY §8(d) "acting-only": S = 0, frozen weights, like
     Simulator.run_simulation): graph -> GAT/GCN Q -> argmax -> env.step for every env, episodes of
@@ -650,30 +724,9 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    d = mean_in_degree(args, eng)
-    if args.net == "gat3":
-        f_node = gat3_fwd_flops(N, d) + 300
-    else:
-        f_node = (gat_fwd_flops(N, d) if args.conv == "gat" else gcn_fwd_flops(N, d)) + 300   # + physics
     roof = None
     if not args.no_kernel_timing:   # one 100-tick rollout launch, HIP events on its stream
-        stream = torch.cuda.current_stream()
-        per = []
-        for _ in range(5):
-            eng.reset()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            eng.rollout(max_steps, eps=0.0)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            per.append(e0.elapsed_time(e1) * 1e-3)
-        t_l = float(np.median(per))
-        flops = B * N * max_steps * f_node
-        ach = flops / t_l / 1e12
-        roof = {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
-                "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / PEAK_FP32_TFLOPS, "traffic": None, "kernel": "act_kernel rollout (swarm_rollout)",
-                "algorithmic_flops_per_launch": flops, "launch_us": round(t_l * 1e6, 2)}
+        roof = rollout_roofline(args, eng, max_steps, acting_fnode(args, eng))
     if rank == 0:
         g = {"complete": "complete", "knn": f"kNN-{args.knn_k}", "radius": f"radius-{args.radius}"}[args.graph]
         line = {"metric": "env-steps/sec (agents×envs), acting-only rollout",

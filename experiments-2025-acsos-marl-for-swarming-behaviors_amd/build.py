@@ -59,10 +59,20 @@ def up_to_date() -> bool:
 STAMPS_OUT = os.path.join(HERE, "libswarm_hip_stamps.so")
 # test-only variant: every fused-tick hand-off wait overruns at once (tests of the drop path)
 HODROP_OUT = os.path.join(HERE, "libswarm_hip_hodrop.so")
+# test-only variant: the target waves' s' waits overrun at once, the online waves' r waits run to
+# their bound (an overrun is counted once per dropping wave, not again by the r wait)
+HODROP2_OUT = os.path.join(HERE, "libswarm_hip_hodrop2.so")
+# test-only variant: 256-thread slab-reduce blocks (16 slab groups), so that eight ranks' peer
+# reduces (each 109 blocks, all waiting on each other) are resident together on ONE GPU
+# (tests/test_gpu_peer.py, the W = 8 fused exchange)
+RED256_OUT = os.path.join(HERE, "libswarm_hip_red256.so")
 # diagnostic variant: in-kernel realtime launch stamps only (tools/tick_split_stamps.py)
 RTSTAMPS_OUT = os.path.join(HERE, "libswarm_hip_rtstamps.so")
 VARIANTS = {"main": (OUT, []), "stamps": (STAMPS_OUT, ["-DSWARM_STAMPS=1"]),
-            "rtstamps": (RTSTAMPS_OUT, ["-DSWARM_STAMPS=2"]), "hodrop": (HODROP_OUT, ["-DSWARM_HO_FORCE_DROP=1"])}
+            "rtstamps": (RTSTAMPS_OUT, ["-DSWARM_STAMPS=2"]), "hodrop": (HODROP_OUT, ["-DSWARM_HO_FORCE_DROP=1"]),
+            "hodrop2": (HODROP2_OUT, ["-DSWARM_HO_FORCE_DROP=2"]), "red256": (RED256_OUT, ["-DSWARM_RED_GROUPS=16"])}
+# the libraries the GPU tests load besides the main one (__graft_entry__.build builds them)
+TEST_VARIANTS = ("hodrop", "hodrop2", "red256")
 
 
 def build(force: bool = False, verbose: bool = True, stamps: bool = False, variant: str = "main",

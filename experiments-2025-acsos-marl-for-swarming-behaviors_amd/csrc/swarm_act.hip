@@ -261,8 +261,13 @@ const char* swarm_build_info(void) {
 #elif SWARM_STAMPS == 2
          " rtstamps"
 #endif
-#if SWARM_HO_FORCE_DROP
+#if SWARM_HO_FORCE_DROP == 1
          " hodrop"
+#elif SWARM_HO_FORCE_DROP == 2
+         " hodrop2"
+#endif
+#ifdef SWARM_RED_GROUPS
+         " redgroups" SWARM_STR(SWARM_RED_GROUPS)
 #endif
       ;
 }

@@ -47,8 +47,11 @@ struct ReduceArgs {
 // and stores the whole ctrl update (Adam scalars of the next step in double, the next
 // tick's sampling key) in parallel with the column blocks, so no column block waits on it.
 // Three more blocks copy w / m / v _nxt -> _cur (one array each), beside the column blocks.
+#ifndef SWARM_RED_GROUPS
+#define SWARM_RED_GROUPS 64   // test builds: 16 (256-thread blocks, so 8 ranks' peer reduces fit one GPU)
+#endif
 constexpr int kRedCols = 16;      // columns per reduce block
-constexpr int kRedGroups = 64;    // slab groups per column (consecutive slabs each)
+constexpr int kRedGroups = SWARM_RED_GROUPS;   // slab groups per column (consecutive slabs each)
 constexpr int kRedRuns = kRedGroups / 8;
 constexpr int kRedChunk = 8;      // slabs per load chunk of a group
 constexpr int kRedColBlocks = (N_PARAMS + 1 + kRedCols - 1) / kRedCols;
@@ -101,6 +104,11 @@ __device__ inline void red_control(swarm_ctrl* C, const RedCtrl& A) {
       C->adam_inv_bc2 = next_inv_bc2;
     }
     C->trained = trained;
+    // (float)(1 - beta) of the Adam step, rewritten every tick from the launch's double
+    // hyper-parameters: a control block that skipped swarm_ctrl_init (zero-filled) has its
+    // first optimizer step pending only after this write, so no step runs with 0 here
+    C->one_m_beta1 = (float)(1.0 - adam_beta1(A.hp));
+    C->one_m_beta2 = (float)(1.0 - adam_beta2(A.hp));
     C->tick = c_tick + 1;
     C->write_slot = (c_slot + 1) % cap;
     C->filled_slots = valid_slots;
@@ -226,7 +234,10 @@ __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
   const uint32_t tick = C->tick;
   const uint32_t step = C->adam_step + 1;
   const float step_size = C->adam_step_size, inv_bc2 = C->adam_inv_bc2;
-  const float one_m_b1 = C->one_m_beta1, one_m_b2 = C->one_m_beta2;
+  // ctrl words 24-25 (swarm_ctrl_init); a control block that skipped it holds 0 there: the
+  // same value from the launch's hyper-parameters instead of freezing m and v
+  const float one_m_b1 = C->one_m_beta1 != 0.0f ? C->one_m_beta1 : (float)(1.0 - adam_beta1(A.hp));
+  const float one_m_b2 = C->one_m_beta2 != 0.0f ? C->one_m_beta2 : (float)(1.0 - adam_beta2(A.hp));
   const bool train = A.flush ? (C->trained != 0u && C->peer_hold == 0u)
                              : (valid_slots * (uint32_t)A.B >= (uint32_t)A.hp.batch);
   // target sync: unfused = after the TD step of tick `tick` ((tick+1) % every); flush = the

@@ -110,7 +110,11 @@ struct TdFused {
 #endif
 constexpr int kHoSpinLimit = SWARM_HO_SPIN_LIMIT;   // polls (with s_sleep) before a hand-off wait gives up
 // test builds only (libswarm_hip_hodrop.so): every hand-off wait overruns at once
-constexpr bool kHoForceDrop = SWARM_HO_FORCE_DROP != 0;
+constexpr bool kHoForceDrop = SWARM_HO_FORCE_DROP == 1;
+// test builds only (libswarm_hip_hodrop2.so): the target waves' s' waits overrun at once and the
+// online waves never see r (their waits run to the bound): an overrun counts once per wave that
+// dropped, not again in the online wave's r wait for a graph its target wave already dropped
+constexpr bool kHoDropTarget = SWARM_HO_FORCE_DROP == 2;
 
 // A hand-off wait that overruns drops the graphs it waited for: their nodes become padding
 // (no TD error, no gradient, no loss), so the update is the mean over the S*N batch nodes with
@@ -302,6 +306,11 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     for (int ct = 0; ct < CT; ++ct)
       if (16 * ct + c < NS) TB.act[row0 + 16 * ct + c] = act[ct];
   }
+  if (FUSED && !online && p == 0) {   // no graph dropped yet (set by an s' overrun, read by the r wait)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      if (16 * ct + c < NS) TB.tdrop[row0 + 16 * ct + c] = 0;
+  }
   __syncthreads();   // B0: weight images
   SWARM_STAMP(2);
   bool pre = false;
@@ -330,17 +339,23 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       for (int ct = 0; ct < CT; ++ct) {
         okc[ct] = true;
         if (ho[ct]) {
-          okc[ct] = !kHoForceDrop && (uint32_t)(g[ct][0] >> 32) == tag && (uint32_t)(g[ct][1] >> 32) == tag &&
-                    (uint32_t)(g[ct][2] >> 32) == tag && (uint32_t)(g[ct][3] >> 32) == tag;
+          okc[ct] = !kHoForceDrop && !(kHoDropTarget && !online) && (uint32_t)(g[ct][0] >> 32) == tag &&
+                    (uint32_t)(g[ct][1] >> 32) == tag && (uint32_t)(g[ct][2] >> 32) == tag &&
+                    (uint32_t)(g[ct][3] >> 32) == tag;
           ok = ok && okc[ct];
           st[ct] = make_float4(__uint_as_float((uint32_t)g[ct][0]), __uint_as_float((uint32_t)g[ct][1]),
                                __uint_as_float((uint32_t)g[ct][2]), __uint_as_float((uint32_t)g[ct][3]));
         }
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
-      if (kHoForceDrop || spin >= kHoSpinLimit) {   // never in a correct run: count it, drop the graphs
-        if (lane == 0) atomicAdd(X.ho_err, 1u);
+      if (kHoForceDrop || (kHoDropTarget && !online) || spin >= kHoSpinLimit) {   // never in a correct
+        if (lane == 0) atomicAdd(X.ho_err, 1u);                                   // run: count, drop
         drop_overrun<NS, GS>(okc, live_drop, nv, c);
+        if (FUSED && !online && p == 0) {   // tell the online waves' r wait (they do not count it again)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            if (16 * ct + c < NS && live_drop[ct]) *(volatile int*)&TB.tdrop[row0 + 16 * ct + c] = 1;
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
@@ -492,15 +507,29 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         okc[ct] = true;
         if (ho[ct] && !live_drop[ct]) {
           const unsigned long long g = ld_granule(ho_at(ct, 8 * N, 1));
-          okc[ct] = !kHoForceDrop && (uint32_t)(g >> 32) == tag;
+          okc[ct] = !kHoForceDrop && !kHoDropTarget && (uint32_t)(g >> 32) == tag;
           ok = ok && okc[ct];
           rew[ct] = __uint_as_float((uint32_t)g);
         }
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
       if (kHoForceDrop || spin >= kHoSpinLimit) {   // the graph's rows are dropped (online side)
-        if (lane == 0) atomicAdd(X.ho_err, 1u);
-        drop_overrun<NS, GS>(okc, live_drop, nv, c);
+        // graphs the target wave has dropped already (its s' wait overran; LDS flag set before its
+        // count) are dropped here too but not counted a second time
+        bool rest = false;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          if (!okc[ct] && *(volatile int*)&TB.tdrop[row0 + min(16 * ct + c, NS - 1)] != 0) {
+            okc[ct] = true;
+            live_drop[ct] = true;
+            nv[ct] = false;
+          }
+          rest = rest || !okc[ct];
+        }
+        if (__builtin_amdgcn_ballot_w64(rest)) {
+          if (lane == 0) atomicAdd(X.ho_err, 1u);
+          drop_overrun<NS, GS>(okc, live_drop, nv, c);
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -91,7 +91,10 @@ typedef struct swarm_ctrl {
                              summed gradient is wrong), so a timeout never reaches the weights.
                              Cleared only by swarm_ctrl_init; PeerExchange.check() raises on it. */
   float one_m_beta1;      /* words 24-25: (float)(1 - beta1), (float)(1 - beta2) formed in double from   */
-  float one_m_beta2;      /* swarm_adam_cfg's double betas by swarm_ctrl_init, as torch forms them   */
+  float one_m_beta2;      /* swarm_adam_cfg's double betas by swarm_ctrl_init, as torch forms them, and
+                             rewritten by every swarm_reduce_advance[_peer]; swarm_adam_step / _flush
+                             form them from their swarm_adam_cfg when a word is 0 (a control block
+                             that skipped swarm_ctrl_init), so no step freezes m and v            */
   uint32_t pad1[6];
 } swarm_ctrl;           /* 32 words */
 /* A fresh control block comes from swarm_ctrl_init (all counters 0, beta powers 1). */

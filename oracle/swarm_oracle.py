@@ -806,6 +806,10 @@ def td_loss_grad(flat_params, flat_target, s_state, actions, rewards, s_next_sta
     inputs: the "exact" value both fp32 paths (this oracle and the GPU) are measured against.
     Returns (loss, flat grad [N_PARAMS], online Q at the taken actions, TD targets).
     """
+    if conv in ("gcn", "gcn_edges", "gat_dense") and (edge_index is not None or edge_index_next is not None):
+        # these restatements build complete graphs themselves: an edge list would be ignored and the
+        # gradient (and any noise bound taken from it) would silently belong to the wrong graph
+        raise ValueError(f"conv={conv!r} restates complete graphs only; edge_index must be None")
     if conv in ("gcn", "gcn_edges"):
         return _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_next_state, gamma, dtype,
                                  edges=conv == "gcn_edges")

@@ -720,6 +720,58 @@ def test_handoff_overrun_drops_the_waiting_graphs(sw, golden_weights):
     assert ((g[:O.N_PARAMS] - ref_grad * frac).abs().max() / gscale).item() < 2e-5
 
 
+def test_handoff_overrun_is_counted_once_per_dropping_wave(sw, golden_weights):
+    """a graph whose target wave dropped it (s' wait overran) must not be counted a
+    second time by its online wave's r wait.  The test library (-DSWARM_HO_FORCE_DROP=2) makes
+    every target wave's s' wait overrun at once and hides r from the online waves, whose waits
+    then run to their bound: the count is one per target wave holding a hand-off graph (at tick 0
+    every graph waits), not two, and every graph is dropped."""
+    from swarm_amd import _lib, build
+    lib = _lib.load_variant(build.HODROP2_OUT)
+    B, N, S, slots = 32, 8, 32, 2
+    p = _params(golden_weights, "go_to", 2)
+    eng = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, batch=S, eps=0.3, replay_capacity=slots * B,
+                         update_target_every=1000)
+    assert eng.fused
+    eng.lib = lib
+    eng.reset(0)
+    eng.train_tick()   # tick 0: every sampled graph comes from the slot being written
+    torch.cuda.synchronize()
+    target_waves = -(-S // 2)   # N <= 8: two graphs per TD wave, one target wave per online wave
+    assert eng.handoff_errors() == target_waves, (eng.handoff_errors(), target_waves)
+    assert torch.count_nonzero(eng.grad.cpu()) == 0   # all graphs dropped: no gradient, no loss
+
+
+def test_adam_step_on_a_control_block_that_skipped_init(sw, golden_weights):
+    """ctrl words 24-25 ((float)(1 - beta)) are written by swarm_ctrl_init.  A zero-filled
+    control block must not freeze m and v: swarm_adam_step forms the words from its hyper-parameters,
+    and the fused tick's reduce rewrites them every tick (the first fused tick of a zero-filled block
+    has no pending step), so both paths equal a properly initialised engine."""
+    from swarm_amd._lib import CTRL
+    p = _params(golden_weights, "go_to", 1)
+    B, N, S = 32, 8, 32
+    kw = dict(seed=8, params=p, batch=S, eps=0.3, replay_capacity=3 * B, update_target_every=1000)
+    for fused in (False, True):
+        a, b = sw.SwarmEngine("GoTo", N, B, **kw), sw.SwarmEngine("GoTo", N, B, **kw)
+        for e in (a, b):
+            e.reset(0)
+            for _ in range(2):
+                e.act(push=True, full_out=False)
+                e.advance()
+        c = b.ctrl.clone()
+        c[CTRL["one_m_beta1"]] = 0
+        c[CTRL["one_m_beta2"]] = 0
+        b.ctrl.copy_(c)
+        for _ in range(3):
+            for e in (a, b):
+                e.train_tick() if fused else e.train_tick_unfused()
+        a.flush()
+        b.flush()
+        torch.cuda.synchronize()
+        assert b.read_ctrl()["adam_step"] >= 2 and bool(b.adam_v.abs().sum() > 0)
+        assert torch.equal(a.params, b.params) and torch.equal(a.adam_m, b.adam_m) and torch.equal(a.adam_v, b.adam_v)
+
+
 def test_trainer_raises_on_handoff_overrun(sw, tmp_path):
     env = sw.make_env(sw.GoToPositionScenario(), num_envs=4, continuous_actions=False, max_steps=5,
                       dict_spaces=True, seed=0, n_agents=5)

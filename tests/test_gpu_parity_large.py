@@ -275,3 +275,41 @@ def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, 
     _end_to_end_weights(f"{name} fused flushed second step", eng.params.cpu(), pw, g32p, mp, vp, sp)
     _adam_check(f"{name} fused flushed second step", eng.params.cpu(), eng.adam_m.cpu(), eng.adam_v.cpu(), pw, ggp,
                 mp, vp, sp)
+
+
+def test_fused_tick_target_sync_at_benchmark_size(sw, golden_weights):
+    """VERDICT r4 "next" #5: the fused tick's target sync (train_gcn_dqn.py:131-133: after the
+    optimizer step of reference tick `ticks`, target <- model when ticks % update_target_every == 0)
+    at C2's size with update_target_every = 2.  The update of tick t is applied in tick t + 1's
+    prologue, which also writes the target row when (t + 1) % every == 0, and that tick's TD blocks
+    already use the synced target.  Checked against the oracle: the synced target equals the
+    post-step weights bit for bit and torch's update on the fp32 oracle's gradient within 2e-6; the
+    next tick's gradient (computed against the synced target) passes the oracle bounds; the tick
+    after it leaves the target alone."""
+    name, scen, N, B, S, conv = "C2 sync", "GoTo", 8, 1024, 1024, "gat"
+    p = _weights(golden_weights, scen, 5)
+    eng = sw.SwarmEngine(scen, N, B, seed=14, params=p, batch=S, replay_capacity=6 * B, eps=0.3,
+                         update_target_every=2, conv=conv)
+    assert eng.fused
+    _prefill(eng, 3)
+    assert eng.read_ctrl()["tick"] == 3
+    t0 = eng.target.cpu().clone()
+    # tick 3: nothing pending yet (prefill does not train), its TD uses the initial target
+    eng.train_tick()
+    torch.cuda.synchronize()
+    p3 = eng.params.cpu().clone()
+    g32, g_gpu = _compare_update(f"{name} tick 3", eng, p3, t0, eng.samples.cpu().clone(), S, N, scen, conv)
+    assert torch.equal(eng.target.cpu(), t0)
+    # tick 4: its prologue applies tick 3's step and syncs (4 % 2 == 0)
+    eng.train_tick()
+    torch.cuda.synchronize()
+    assert eng.handoff_errors() == 0
+    w4, tgt4 = eng.params.cpu().clone(), eng.target.cpu().clone()
+    assert not torch.equal(w4, p3) and torch.equal(tgt4, w4), "the target row is the post-step weights"
+    _end_to_end_weights(f"{name} synced target", tgt4, p3, g32, None, None, 0)
+    _adam_check(f"{name} synced target", tgt4, eng.adam_m.cpu(), eng.adam_v.cpu(), p3, g_gpu, None, None, 0)
+    _compare_update(f"{name} tick 4 (synced target)", eng, w4, tgt4, eng.samples.cpu().clone(), S, N, scen, conv)
+    # tick 5: step applied, no sync (5 % 2 != 0)
+    eng.train_tick()
+    torch.cuda.synchronize()
+    assert not torch.equal(eng.params.cpu(), w4) and torch.equal(eng.target.cpu(), tgt4)
