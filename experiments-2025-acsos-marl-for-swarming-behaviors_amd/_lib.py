@@ -22,11 +22,14 @@ F_SHARED_RESET, F_RANDOM_OA = 1, 2
 N_PARAMS = 1673
 NET_GCN, NET_GAT3 = 0, 1
 GAT3_N_PARAMS = 409
+GRAD_FLOATS = 1792        # SWARM_GRAD_FLOATS: gradient, loss sum, the clip norm's group partials
+GRAD_SQ_BASE = 1680       # SWARM_GRAD_SQ_BASE
+ADAM_F_NORM_PARTIALS = 1  # swarm_adam_cfg.flags
 ERRORS = {-1: "SWARM_E_BADARG (invalid shape/config)",
           -2: "selected index k out of range (SWARM_E_KNN_K)",
           -3: "SWARM_E_NOGPU",
           -4: "SWARM_E_UNSUPPORTED (no fused-tick kernel for this configuration)"}
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class SwarmConfig(ctypes.Structure):
@@ -48,7 +51,7 @@ class SwarmActOut(ctypes.Structure):
 class SwarmAdamCfg(ctypes.Structure):
     _fields_ = [("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float),
                 ("max_norm", c_float), ("gamma", c_float), ("batch", c_int32),
-                ("update_target_every", c_int32), ("world_size", c_int32), ("pad", c_int32),
+                ("update_target_every", c_int32), ("world_size", c_int32), ("flags", c_int32),
                 ("lr_d", ctypes.c_double), ("beta1_d", ctypes.c_double), ("beta2_d", ctypes.c_double)]
 
 

@@ -56,7 +56,7 @@ template <int NS>
 struct ActSmem {
   WScratch<NS> SW[kActWPB];
   __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
-  float red[8 * kActWPB + 8];
+  float red[64];   // the optimizer step's norm (adam_norm2_block)
 };
 
 // vb / nvb: this block's index among the nvb acting blocks of the launch (the fused
@@ -101,7 +101,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // of anything that waits on ctrl or the kernarg segment
   constexpr bool kLearnCT = MODE == MODE_TICK && NET == SWARM_NET_GCN && HO;
   AdamRegs R;
-  if (kLearnCT) R.load(grad, w_cur, m_cur, v_cur, threadIdx.x);
+  if (kLearnCT) R.load(grad, w_cur, m_cur, v_cur, threadIdx.x, true);
   DFwd<NS> F;
   float px[CT], py[CT], vx[CT], vy[CT];
   bool valid[CT];
@@ -181,13 +181,15 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
     const int tid = threadIdx.x;
-    if (!kLearnCT) R.load(grad, w_cur, m_cur, v_cur, tid);
+    if (!kLearnCT) R.load(grad, w_cur, m_cur, v_cur, tid, true);
     const uint32_t pending = cc.peer_hold ? 0u : cc.trained;   // a held rank applies no step
     const uint32_t tnow = cc.tick;
     const float step_size = cc.adam_step_size, inv_bc2 = cc.adam_inv_bc2;
     float gn = 0.0f;
     SWARM_STAMP(20);
-    if (pending) gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, cc.one_m_beta1, cc.one_m_beta2, tid, red);
+    if (pending)
+      gn = adam_apply<21>(R, A.hp, step_size, inv_bc2, cc.one_m_beta1, cc.one_m_beta2, tid, red,
+                          (A.hp.flags & SWARM_ADAM_F_NORM_PARTIALS) != 0);
     store_w_lds(Pw, R, tid);
     SWARM_STAMP(24);
     if (vb == 0) {

@@ -11,6 +11,15 @@
 // single_tensor: m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g g; denom = sqrt(v)/sqrt(bc2) + eps;
 // w += -(lr/bc1) * m/denom.  bc = 1 - beta^step with beta^step kept as a running
 // double product in the control block (python's beta ** step up to ~1e-16 relative).
+//
+// The squared global norm has ONE fixed summation order on every path (ABI 10, swarm_hip.h
+// SWARM_GRAD_SQ_BASE): per float4 i of parameters 4i..4i+3, d[i] = ((g0^2 + g1^2) + g2^2) + g3^2
+// (the tail parameter 1672 alone in d[418]); per group j of four float4s (16 parameters),
+// sq[j] = (d[4j] + d[4j+1]) + (d[4j+2] + d[4j+3]); then wave_sum over lanes l = 0..63 of
+// sq[l] + sq[l + 64].  The slab reduce forms sq[j] for its 16 columns as it writes them, so the
+// fused tick's prologue (SWARM_ADAM_F_NORM_PARTIALS) loads 105 partials with its other operands
+// and every wave forms the norm alone, with no block barrier in front of the Adam elements;
+// without the flag (and in swarm_adam_step / _flush) the block forms the same sums from grad.
 #pragma once
 #include "swarm_common.h"
 
@@ -20,6 +29,12 @@ constexpr int kAdamNT = 256;                           // threads of every Adam 
 constexpr int kAdamNF4 = N_PARAMS / 4;                 // 418 float4 = floats 0..1671
 constexpr int kAdamNJ = (kAdamNF4 + kAdamNT - 1) / kAdamNT;
 static_assert(kAdamNF4 * 4 + 1 == N_PARAMS, "one tail element (lin2.bias[8])");
+constexpr int kGradSqBase = SWARM_GRAD_SQ_BASE;     // the norm's group partials in a grad buffer
+constexpr int kGradSqCount = SWARM_GRAD_SQ_COUNT;   // 105 groups of 16 parameters
+static_assert(kGradSqCount == (N_PARAMS + 15) / 16 && kGradSqCount > 64 && kGradSqCount <= 128, "norm groups");
+static_assert(kGradSqBase >= N_PARAMS + 1 && kGradSqBase % 16 == 0 && kGradSqBase + 112 <= SWARM_GRAD_FLOATS,
+              "grad buffer layout");
+static_assert(kAdamNJ == 2 && kAdamNT == 256, "a thread's float4s i = tid and 256 + tid: groups tid/4 and 64 + tid/4");
 
 // beta^step running products live in the control block (two doubles, words 10-13)
 __device__ inline double ctrl_get_double(const swarm_ctrl* c, int word) {
@@ -61,10 +76,12 @@ __device__ inline void ctrl_store_next_scalars(swarm_ctrl* c, const swarm_adam_c
 struct AdamRegs {
   float4 g[kAdamNJ], w[kAdamNJ], m[kAdamNJ], v[kAdamNJ];
   float gt, wt, mt, vt;    // tail element N_PARAMS - 1
+  float sq_lo, sq_hi;      // the reduce's norm partials sq[lane], sq[lane + 64] (0 past the last)
 
-  // every load issued unconditionally (clamped index): one memory round trip
+  // every load issued unconditionally (clamped index): one memory round trip.  partials: also
+  // load the slab reduce's norm partials (grad + kGradSqBase)
   __device__ inline void load(const float* __restrict__ grad, const float* __restrict__ w_, const float* __restrict__ m_,
-                              const float* __restrict__ v_, int tid) {
+                              const float* __restrict__ v_, int tid, bool partials = false) {
 #pragma unroll
     for (int j = 0; j < kAdamNJ; ++j) {
       const int i = min(tid + kAdamNT * j, kAdamNF4 - 1);
@@ -82,6 +99,13 @@ struct AdamRegs {
     gfloat* tv = (gfloat*)(v_ + (N_PARAMS - 1));
     asm volatile("" : "+v"(tg), "+v"(tw), "+v"(tm), "+v"(tv));
     gt = *tg; wt = *tw; mt = *tm; vt = *tv;
+    sq_lo = 0.0f; sq_hi = 0.0f;
+    if (partials) {
+      const int l = tid & 63;
+      sq_lo = grad[kGradSqBase + l];
+      const float hi = grad[kGradSqBase + min(l + 64, kGradSqCount - 1)];
+      sq_hi = l + 64 < kGradSqCount ? hi : 0.0f;
+    }
   }
 };
 
@@ -115,40 +139,57 @@ __device__ inline void adam_elem(float g, float& w, float& m, float& v, float on
   w = w + (-step_size) * (m * __builtin_amdgcn_rcpf(denom));
 }
 
-// One optimizer step in registers by the whole workgroup (kAdamNT threads; contains
-// __syncthreads).  step_size / inv_bc2_sqrt: ctrl's scalars of this step.  Returns the
-// pre-clip global norm.  red: LDS scratch of >= kAdamNT/64 floats.
+// ---- the squared norm in the canonical order (header comment)
+// world_size > 1: the summed gradient divided by W first (every path alike)
+__device__ inline void adam_scale(AdamRegs& R, const swarm_adam_cfg& hp) {
+  if (hp.world_size > 1) {
+    const float inv_w = 1.0f / (float)hp.world_size;
+#pragma unroll
+    for (int j = 0; j < kAdamNJ; ++j) {
+      float4 g = R.g[j];
+      g.x = g.x * inv_w; g.y = g.y * inv_w; g.z = g.z * inv_w; g.w = g.w * inv_w;
+      R.g[j] = g;
+    }
+    R.gt = R.gt * inv_w;
+  }
+}
+// d[i] of float4 i = tid + 256 j (the tail parameter alone in d[418], 0 past it)
+__device__ inline float norm_d(const AdamRegs& R, int j, int tid) {
+  const int i = tid + kAdamNT * j;
+  const float4 g = R.g[j];
+  const float d = ((g.x * g.x + g.y * g.y) + g.z * g.z) + g.w * g.w;
+  return i < kAdamNF4 ? d : (i == kAdamNF4 ? R.gt * R.gt : 0.0f);
+}
+// group sum of a quad of lanes (xor 1, then xor 2): (d0 + d1) + (d2 + d3) in every lane of the quad
+__device__ inline float quad_sum(float x) {
+  x = x + adam_dpp<0xB1>(x);
+  return x + adam_dpp<0x4E>(x);
+}
+// the block forms the partials from its float4s (one barrier): red >= 64 floats
+__device__ inline float adam_norm2_block(const AdamRegs& R, int tid, float* red) {
+  const float p = quad_sum(norm_d(R, 0, tid)) + quad_sum(norm_d(R, 1, tid));   // sq[tid/4] + sq[64 + tid/4]
+  if ((tid & 3) == 0) red[tid >> 2] = p;
+  __syncthreads();
+  return wave_sum(red[tid & 63]);
+}
+// SWARM_ADAM_F_NORM_PARTIALS: every wave from the reduce's partials, no barrier
+__device__ inline float adam_norm2_partials(const AdamRegs& R) { return wave_sum(R.sq_lo + R.sq_hi); }
+
+// One optimizer step in registers by the whole workgroup (kAdamNT threads).  step_size /
+// inv_bc2_sqrt: ctrl's scalars of this step.  partials: the squared norm from R.sq_lo / sq_hi
+// (loaded with partials = true; no barrier), else formed by the block (contains __syncthreads;
+// red: LDS scratch of >= 64 floats).  Returns the pre-clip global norm.
 template <int SB = -1>   // SB: diagnostic stamp base (SWARM_STAMPS builds only)
 // one_m_b1 / one_m_b2: ctrl's (float)(1 - beta) (swarm_ctrl_init, from the double betas): read
 // with the control block the prologue loads anyway, not from a kernarg double on its chain
 __device__ inline float adam_apply(AdamRegs& R, const swarm_adam_cfg& hp, float step_size, float inv_bc2_sqrt,
-                                   float one_m_b1, float one_m_b2, int tid, float* red) {
+                                   float one_m_b1, float one_m_b2, int tid, float* red, bool partials = false) {
 #define AD_STAMP(i) do { if (SB >= 0) SWARM_STAMP(SB + (i)); } while (0)
-  const float inv_w = 1.0f / (float)hp.world_size;
+  adam_scale(R, hp);
+  AD_STAMP(0);
   // clip_grad_norm_: the norm of the per-tensor norms == the global L2 norm up to rounding
   // (<= ~1e-7 relative on the clip coefficient); one fixed-order reduction
-  float ss = 0.0f;
-#pragma unroll
-  for (int j = 0; j < kAdamNJ; ++j) {
-    const int i = tid + kAdamNT * j;
-    float4 g = R.g[j];
-    if (hp.world_size > 1) { g.x = g.x * inv_w; g.y = g.y * inv_w; g.z = g.z * inv_w; g.w = g.w * inv_w; }
-    R.g[j] = g;
-    const float d = ((g.x * g.x + g.y * g.y) + g.z * g.z) + g.w * g.w;
-    ss = ss + (i < kAdamNF4 ? d : 0.0f);
-  }
-  if (hp.world_size > 1) R.gt = R.gt * inv_w;
-  if (tid == 0) ss = ss + R.gt * R.gt;
-  AD_STAMP(0);
-  constexpr int NW = kAdamNT / 64;
-  {
-    const float s = wave_sum(ss);
-    if ((tid & 63) == 0) red[tid >> 6] = s;
-  }
-  __syncthreads();
-  float nn = red[0];
-#pragma unroll
-  for (int w = 1; w < NW; ++w) nn = nn + red[w];
+  const float nn = partials ? adam_norm2_partials(R) : adam_norm2_block(R, tid, red);
   // v_sqrt_f32 and a reciprocal multiply (<= 1 ulp each) instead of the correctly rounded
   // expansions: the clip coefficient is a serial chain every prologue waits on (0.075 us per
   // tick at C2, profiles/r02_ab_wpe.jsonl)

@@ -122,6 +122,7 @@ __device__ inline void red_control(swarm_ctrl* C, const RedCtrl& A) {
 
 static_assert(kRedGroups % 8 == 0 && kRedCols * kRedGroups <= 1024, "reduce geometry");
 static_assert(kRedColBlocks <= kPeerSeqRegion, "peer seq region");
+static_assert(kRedColBlocks == kGradSqCount && kRedCols == 16, "one norm partial per column block");
 // slabs / ctrl / geometry preloaded into SGPRs (kernarg preload): the slab loads issue at wave start.
 // PEER = 1 (swarm_reduce_advance_peer): each column block then exchanges its 16 column sums with
 // the other ranks (swarm_peer.h) and writes grad = their rank-ordered sum: the all-reduce costs
@@ -132,6 +133,7 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   __shared__ float part[kRedGroups][kRedCols];
   __shared__ float part2[kRedRuns][kRedCols];
   __shared__ float peer_rv[PEER ? SWARM_PEER_MAX : 1][kRedCols];
+  __shared__ float sqv[kRedCols];
   SWARM_RTSTAMP(22);
   SWARM_STAMP(28);
   swarm_ctrl* C = ctrl;
@@ -185,12 +187,14 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     part2[q][c] = r;
   }
   __syncthreads();
+  float gcol = 0.0f;   // q == 0: this column's gradient as written to grad
   if (q == 0 && col <= N_PARAMS) {
     float tot = part2[0][c];
 #pragma unroll
     for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
     if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
     else A.grad[col] = tot;
+    gcol = tot;
     // this rank's loss of the update (0 when skipped: the TD launch wrote zero slabs)
     if (advance && col == N_PARAMS) C->loss = tot / (float)((size_t)A.batch * A.N);
   }
@@ -201,7 +205,23 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
       float tot = peer_rv[0][c];
       for (int w = 1; w < A.peer.world_size; ++w) tot = tot + peer_rv[w][c];
       A.grad[col] = tot;
+      gcol = tot;
     }
+  }
+  // the clip norm's partial of these 16 columns = parameter group blockIdx.x (swarm_adam.h):
+  // lanes 0-15 of wave 0 hold the columns; squares as the optimizer step forms them (scaled by
+  // 1/W first when W > 1), the float4 sums ((a + b) + c) + d by lanes 0-3, then their quad sum
+  if (q == 0) {
+    float g = col < N_PARAMS ? gcol : 0.0f;
+    if (A.hp.world_size > 1) g = g * (1.0f / (float)A.hp.world_size);
+    sqv[c] = g * g;
+  }
+  wave_lds_sync();   // sqv is written and read by wave 0 only
+  if (threadIdx.x < 4) {
+    const int f = threadIdx.x;
+    const float d = ((sqv[4 * f] + sqv[4 * f + 1]) + sqv[4 * f + 2]) + sqv[4 * f + 3];
+    const float sq = quad_sum(d);
+    if (f == 0) A.grad[kGradSqBase + blockIdx.x] = sq;
   }
   SWARM_STAMP(31);
   SWARM_RTSTAMP(23);
@@ -222,7 +242,7 @@ struct AdamArgs {
 };
 
 __global__ __launch_bounds__(kAdamNT) void adam_kernel(AdamArgs A) {
-  __shared__ float red[8 * (kAdamNT / 64) + 8];
+  __shared__ float red[64];
   const int tid = threadIdx.x;
   AdamRegs R;
   R.load(A.grad, A.params, A.m, A.v, tid);

@@ -87,7 +87,7 @@ struct TdSmem {
   TdLds<NS> TB;
   __attribute__((aligned(16))) float Pon[N_LDS_PARAMS];
   __attribute__((aligned(16))) float Ptg[N_LDS_PARAMS];
-  float red[8 * 4 + 8];   // fused tick: the Adam norm partials
+  float red[64];   // fused tick: the optimizer step's norm (adam_norm2_block)
 };
 
 // the TD half of the fused training tick (swarm_tick.hip): weights from the pending
@@ -192,7 +192,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   if (FUSED) {   // the fused kernel's preloaded argument SGPRs (== X.lr / A.ctrl): no kernarg round trip first
     cc = *ctrl_pre;   // issued before any kernarg-segment load, so no wait on one delays it
     __builtin_amdgcn_sched_barrier(0);
-    R.load(g_pre, w_pre, m_pre, v_pre, threadIdx.x);
+    R.load(g_pre, w_pre, m_pre, v_pre, threadIdx.x, true);
     __builtin_amdgcn_sched_barrier(0);   // every Adam operand load issued before the first scalar wait
   }
   // fused: the scalars the sampling, the hand-off test and the optimizer step read (ctrl's
@@ -293,7 +293,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   if (FUSED) {   // the pending optimizer step (train_gcn_dqn.py:125-133), as every acting block does;
                  // done before any hand-off wait so that none of it follows the wait
     const bool pending = cc.trained != 0u && cc.peer_hold == 0u;   // a held rank applies no step
-    if (pending) adam_apply(R, hp, cc.adam_step_size, cc.adam_inv_bc2, cc.one_m_beta1, cc.one_m_beta2, threadIdx.x, L.red);
+    if (pending)
+      adam_apply(R, hp, cc.adam_step_size, cc.adam_inv_bc2, cc.one_m_beta1, cc.one_m_beta2, threadIdx.x, L.red,
+                 (hp.flags & SWARM_ADAM_F_NORM_PARTIALS) != 0);
     store_w_lds(Pon, R, threadIdx.x);
     if (pending && (cc.tick % (uint32_t)hp.update_target_every) == 0u) store_w_lds(Ptg, R, threadIdx.x);
     else ptg.store(Ptg, threadIdx.x);

@@ -179,7 +179,7 @@ class SwarmEngine:
             check(int(ws), "swarm_td_workspace_floats")
         self.fused = learn and bool(self.lib.swarm_train_tick_supported(ctypes_ref(self.cfg)))
         self.slabs = torch.zeros(int(ws), **f32)
-        self.grad = torch.zeros(N_PARAMS + 3, **f32)
+        self.grad = torch.zeros(_lib.GRAD_FLOATS, **f32)   # + the reduce's norm partials (ABI 10)
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
         # fused-tick workspace (error word, launch counters, hand-off granule records); zeroed with ctrl
@@ -268,8 +268,14 @@ class SwarmEngine:
         check(self.lib.swarm_grad_reduce(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
+    def _sync_flags(self):
+        """swarm_adam_cfg.flags for the next launches: the reduce's clip-norm partials describe
+        lr->grad unless an all-reduce of the gradient (RCCL / gloo / by hand) follows the reduce."""
+        exact = self.world_size == 1 or self.peer is not None
+        self.hp.flags = _lib.ADAM_F_NORM_PARTIALS if exact else 0
+
     def allreduce_grad(self):
-        g = self.grad if self.peer is None else self.grad[:N_PARAMS + 1]   # parameters + loss sum
+        g = self.grad[:N_PARAMS + 1]   # parameters + loss sum (not the norm partials)
         allreduce_grad_(g, self.world_size, self.process_group, self.peer)
 
     def adam(self):
@@ -295,6 +301,7 @@ class SwarmEngine:
 
     # single launches of the fused tick (bench.py times each kernel as a back-to-back chain)
     def launch_train_act(self):
+        self._sync_flags()
         check(self.lib.swarm_train_act_step(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
                                             ptr(self.state), ctypes_ref(self.replay), ptr(self.ctrl),
                                             ctypes_ref(self.out_min), ptr(self.samples), stream_ptr()),
@@ -311,6 +318,7 @@ class SwarmEngine:
 
     def launch_tick(self, full_out: bool = False):
         """The fused tick's launch (acting + TD blocks); swarm_reduce_advance follows it."""
+        self._sync_flags()
         check(self.lib.swarm_train_tick(ctypes_ref(self.cfg), ctypes_ref(self.hp), ctypes_ref(self.learner),
                                         ptr(self.state), ctypes_ref(self.replay), ptr(self.ctrl),
                                         ctypes_ref(self.out if full_out else self.out_min), ptr(self.slabs),
@@ -358,6 +366,7 @@ class SwarmEngine:
 
     def train_tick3(self, full_out: bool = False):
         """3-launch training tick: act (+ this tick's TD batch indices), TD, reduce."""
+        self._sync_flags()
         cfg, hp = ctypes_ref(self.cfg), ctypes_ref(self.hp)
         check(self.lib.swarm_train_act_step(cfg, hp, ctypes_ref(self.learner), ptr(self.state),
                                             ctypes_ref(self.replay), ptr(self.ctrl),

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 9
+#define SWARM_ABI_VERSION 10
 
 #define SWARM_E_BADARG (-1)    /* invalid shape / config */
 #define SWARM_E_KNN_K (-2)     /* k > n_agents: torch.topk "selected index k out of range" */
@@ -132,18 +132,38 @@ typedef struct swarm_adam_cfg {
   int32_t batch;                 /* sampled graphs per update (reference 32)       */
   int32_t update_target_every;   /* 200 at train_gcn_dqn.py:175                   */
   int32_t world_size;            /* ranks whose gradients are summed (grad /= W)   */
-  int32_t pad;
+  int32_t flags;                 /* SWARM_ADAM_F_* (ABI 10; was padding)           */
   /* the same lr / betas in double, as torch.optim.Adam holds them (Python floats): 1 - beta
      (into the control block by swarm_ctrl_init) and the bias corrections are formed from these
      as torch forms them (ABI 9); 0 = use the float fields */
   double lr_d, beta1_d, beta2_d;
 } swarm_adam_cfg;
 
+/* swarm_adam_cfg.flags.  SWARM_ADAM_F_NORM_PARTIALS: the clip norm's group partials in lr->grad
+ * (SWARM_GRAD_SQ_BASE, written by the slab reduce) belong to lr->grad as it is: the launch's
+ * optimizer step then reads those 105 values instead of reducing the whole gradient behind a
+ * block barrier (swarm_train_tick, swarm_train_act_step).  Set it when nothing changed lr->grad
+ * after swarm_reduce_advance / _peer (one rank, or the fused peer exchange); clear it when an
+ * all-reduce of the gradient (RCCL) or a caller wrote lr->grad in between.  Both ways give the
+ * same bits: the partials are the same fixed-order sums the step forms otherwise. */
+#define SWARM_ADAM_F_NORM_PARTIALS 1
+
+/* Gradient buffers (swarm_learner.grad, the grad of swarm_grad_reduce / swarm_adam_step) hold
+ * SWARM_GRAD_FLOATS floats: [0, N_PARAMS) the gradient, [N_PARAMS] the sum of squared TD errors,
+ * then at SWARM_GRAD_SQ_BASE the clip norm's 105 group partials the slab reduce writes beside the
+ * gradient (ABI 10): partial j = (d[4j] + d[4j+1]) + (d[4j+2] + d[4j+3]) over the float4 groups
+ * d[i] = ((g0^2 + g1^2) + g2^2) + g3^2 of parameters 4i..4i+3 (each g scaled by 1/world_size when
+ * world_size > 1; parameters >= N_PARAMS count 0); the squared norm is then
+ * wave_sum(partial[l] + partial[l + 64]) over lanes l = 0..63 (swarm_adam.h). */
+#define SWARM_GRAD_SQ_BASE 1680
+#define SWARM_GRAD_SQ_COUNT 105
+#define SWARM_GRAD_FLOATS 1792
+
 /* Learner state for the fused training tick.  Weights/moments are ping-ponged so
  * that every block of swarm_train_act_step can read the previous tick's values
  * while block 0 persists the new ones: tick t reads *_cur, writes *_nxt;
  * swarm_reduce_advance copies *_nxt back to *_cur.  All buffers hold N_PARAMS
- * floats (grad: N_PARAMS + 1, the last = sum of squared TD errors). */
+ * floats (grad: SWARM_GRAD_FLOATS, see above). */
 typedef struct swarm_learner {
   float* w_cur;
   float* w_nxt;
@@ -318,7 +338,8 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
                   const float* target, const swarm_replay* replay, const swarm_ctrl* ctrl,
                   const int32_t* sample_in, int32_t* sample_out, float* slabs, void* stream);
 
-/* Deterministic fixed-order sum of the slabs -> grad[N_PARAMS + 1] (last = loss sum). */
+/* Deterministic fixed-order sum of the slabs -> grad[N_PARAMS + 1] (last = loss sum), plus the
+ * clip norm's group partials at SWARM_GRAD_SQ_BASE (grad holds SWARM_GRAD_FLOATS floats). */
 int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
                       float* grad, void* stream);
 

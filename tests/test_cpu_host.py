@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     for n in sorted(names):
         assert hasattr(raw, n), n
     assert names == set(L.EXPORTED)
-    assert lib.swarm_abi_version() == L.ABI_VERSION == 9 and lib.swarm_n_params() == O.N_PARAMS
+    assert lib.swarm_abi_version() == L.ABI_VERSION == 10 and lib.swarm_n_params() == O.N_PARAMS
 
 
 def test_topk_emulation_matches_torch_fixture():
