@@ -55,6 +55,10 @@ constexpr int kActWPB = 4;   // waves (= environments) per act block; the block 
 template <int NS>
 struct ActSmem {
   WScratch<NS> SW[kActWPB];
+  // per wave (<= 8 slots): the tick's pair forces [NS][NS][2], formed from the positions the wave
+  // loaded while the prologue's optimizer operands are still in flight (they depend on no weight
+  // and no action); 16-slot kernels form them after the argmax in the free H rows instead
+  __attribute__((aligned(16))) float FB[kActWPB][NS <= 8 ? 2 * NS * (NS + 1) : 4];
   __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
   float red[64];   // the optimizer step's norm (adam_norm2_block)
 };
@@ -100,12 +104,12 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // (HO), so its optimizer-step operands are loaded first, from the preloaded pointers, ahead
   // of anything that waits on ctrl or the kernarg segment
   constexpr bool kLearnCT = MODE == MODE_TICK && NET == SWARM_NET_GCN && HO;
-  AdamRegs R;
-  if (kLearnCT) R.load(grad, w_cur, m_cur, v_cur, threadIdx.x, true);
   DFwd<NS> F;
   float px[CT], py[CT], vx[CT], vy[CT];
   bool valid[CT];
   size_t node[CT];
+  // the state first: the pair forces below need only it, and run while the optimizer operands
+  // (issued right after) are in flight
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const int n = 16 * ct + c;
@@ -120,6 +124,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       if (valid[ct]) { px[ct] = st.x; py[ct] = st.y; vx[ct] = st.z; vy[ct] = st.w; }
     }
   }
+  AdamRegs R;
+  if (kLearnCT) R.load(grad, w_cur, m_cur, v_cur, threadIdx.x, true);
   // Flocking: the scenario's per-agent previous_distance_to_agents (flocking_scenario.py:110-122,
   // 163-164), kept after the [B][N][4] state as [B][N] floats (swarm_hip.h, swarm_env_reset)
   float* fl_prev = (SCEN == SWARM_FLOCKING && MODE != MODE_Q) ? state + (size_t)B * N * 4 : nullptr;
@@ -177,6 +183,52 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
         st_granule(ho_r + 4 * (16 * ct + c) + p, ho_tag,
                    __float_as_uint(p == 0 ? px[ct] : (p == 1 ? py[ct] : (p == 2 ? vx[ct] : vy[ct]))));
   }
+  // ---- VMAS pair forces of this tick's positions (World._get_constraint_forces): they need no
+  //      weight and no action, so the first tick's are formed here, while the optimizer operands
+  //      are in flight, instead of between the argmax and the integrator.  64 / NS lanes per agent
+  //      (NS = 8: one pair per lane), each pair into FB[n][u]; the force sum after the argmax adds
+  //      them in VMAS order.  -f(p_u - p_v) == f(p_v - p_u) bit for bit.
+  constexpr bool kHoist = NS <= 8 && NET == SWARM_NET_GCN;
+  // pair-force scratch: FB (hoisted), else the H / T / R rows, free after the forward
+  float* fb = kHoist ? S.FB[w] : &SW[w].H[0][0];
+  // row n of the force matrix at a stride of NS + 1 float2: the force sum's 16 lanes (one agent
+  // each) read 16 distinct LDS banks instead of 2 (a stride of 2 NS floats is a multiple of 32)
+  constexpr int kFbRow = 2 * (NS + 1);
+  static_assert(3 * NS * kRow >= kFbRow * NS, "pair-force scratch");
+  auto pair_forces = [&]() {
+    if (kHoist || MODE == MODE_STEP) {   // else the forward left the positions in sm.px / sm.py
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        if (16 * ct + c < NS && p == 0) { sm.px[16 * ct + c] = px[ct]; sm.py[16 * ct + c] = py[ct]; }
+      wave_lds_sync();
+    }
+    constexpr int LPN = 64 / NS;
+    const int n = d.lane / LPN;
+    const float pxn = sm.px[n], pyn = sm.py[n];
+#pragma unroll
+    for (int j = 0; j < NS / LPN; ++j) {
+      const int u = d.lane % LPN + LPN * j;
+      float gx = 0.0f, gy = 0.0f;
+      if (u < N && n < N) pair_force(pxn - sm.px[u], pyn - sm.py[u], gx, gy);   // u == n: exactly 0
+      *reinterpret_cast<float2*>(fb + n * kFbRow + 2 * u) = make_float2(gx, gy);
+    }
+  };
+  // hoisted for graphs of <= 8 agents (one pair per lane); with 16 slots (4 pairs per lane) the
+  // same hoist measured slower at C3 (18.17 -> 18.82 us per tick, 66 instead of 45 SGPR spills:
+  // profiles/r05_ab_hoist_forces_c3.jsonl), so there the forces keep their place after the argmax
+  if (MODE != MODE_Q && kHoist) pair_forces();
+  // ...and the first tick's random actions of an exploring env (train_gcn_dqn.py:164-165)
+  int ract0[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    ract0[ct] = 0;
+    if (kHoist && explore0) {
+      const int agent = min(16 * ct + c, N - 1);
+      const u32x4 wd = philox4x32(tick, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
+      const int j = agent & 3;
+      ract0[ct] = uniform_int(j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w)), kActions);
+    }
+  }
   if (MODE == MODE_TICK && NET == SWARM_NET_GCN && (kLearnCT || A.learn)) {
     // fused optimizer step of the previous tick's TD gradient (train_gcn_dqn.py:125-133)
     static_assert(64 * kActWPB == kAdamNT, "the act block is one Adam workgroup");
@@ -214,13 +266,12 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   float rew_sum[CT], hits_sum = 0.0f;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) rew_sum[ct] = 0.0f;
-  float* fb = &SW[w].H[0][0];   // pair-force scratch [NS][NS][2] (H/T/R rows are free after the forward)
-  static_assert(3 * NS * kRow >= 2 * NS * NS, "pair-force scratch");
 
   for (int it = 0; it < n_ticks; ++it) {
 #if SWARM_STAMPS == 1   // stamps build: the wave's slowest tick (slot 25 cycles, slot 19 tick index)
     const long long t_tick0 = clock64();
 #endif
+    if (MODE != MODE_Q && kHoist && it > 0) pair_forces();   // this tick's positions
     if (MODE != MODE_Q) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
@@ -232,11 +283,6 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       gat3_forward<NS>(P, d, N, graph, A.k, A.radius, A.dense, V, F);
     } else if (MODE != MODE_STEP) {
       dl_forward<NS, 8>(P, d, N, graph, A.k, A.radius, conv, A.dense, V, false, F);
-    } else {
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct)
-        if (16 * ct + c < NS && p == 0) { sm.px[16 * ct + c] = px[ct]; sm.py[16 * ct + c] = py[ct]; }
-      wave_lds_sync();
     }
     if (it == 0) SWARM_STAMP(2);
 
@@ -257,11 +303,15 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     for (int ct = 0; ct < CT; ++ct) {
       const int agent = min(16 * ct + c, N - 1);
       action[ct] = (MODE == MODE_STEP) ? (valid[ct] ? A.actions[node[ct]] : 0) : argmax9(F.q[ct]);
-      if (explore) {   // the action draw only runs on exploring envs
-        const u32x4 wd = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
-        const int j = agent & 3;
-        const uint32_t word = j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w));
-        action[ct] = uniform_int(word, kActions);
+      if (explore) {   // the action draw only runs on exploring envs (the first tick's: drawn above)
+        if (kHoist && it == 0) {
+          action[ct] = ract0[ct];
+        } else {
+          const u32x4 wd = philox4x32(tk, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
+          const int j = agent & 3;
+          const uint32_t word = j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w));
+          action[ct] = uniform_int(word, kActions);
+        }
       }
     }
 
@@ -279,18 +329,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     //      split its partner pairs (group p: partners p, p + 4, ...), then every lane sums
     //      the forces in VMAS order: 0 + u, obstacle pair, agent pairs in ascending partner
     //      index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
-    {   // pair mapping independent of the D layout: 64 / NS lanes per agent (NS = 8: one pair per lane)
-      constexpr int LPN = 64 / NS;
-      const int n = d.lane / LPN;
-      const float pxn = sm.px[n], pyn = sm.py[n];
-#pragma unroll
-      for (int j = 0; j < NS / LPN; ++j) {
-        const int u = d.lane % LPN + LPN * j;
-        float gx = 0.0f, gy = 0.0f;
-        if (u < N && n < N) pair_force(pxn - sm.px[u], pyn - sm.py[u], gx, gy);   // u == n: exactly 0
-        *reinterpret_cast<float2*>(fb + 2 * (n * NS + u)) = make_float2(gx, gy);
-      }
-    }
+    if (MODE != MODE_Q && !kHoist) pair_forces();   // (16 slots: here, after the argmax)
     if (it == 0) SWARM_STAMP(6);
     wave_lds_sync();
     if (it == 0) SWARM_STAMP(7);
@@ -309,7 +348,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       // (started from +0 or +-1) never become -0, so adding them is exact
       float2 f[NS];
 #pragma unroll
-      for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + 2 * (n * NS + u));
+      for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + n * kFbRow + 2 * u);
 #pragma unroll
       for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
       o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);

@@ -8,4 +8,7 @@ timeout -k 10 1000 python -u tools/ab_trees.py gpurun_out/ab_c2.jsonl ${ROUNDS:-
 if [ -n "$C3" ]; then
 timeout -k 10 1000 python -u tools/ab_trees.py gpurun_out/ab_c3.jsonl ${C3} $V --steps 20 --no-cpu-baseline --scenario ObstacleAvoidance --agents 12 || exit $?
 fi
+if [ -n "$C5" ]; then
+timeout -k 10 1000 python -u tools/ab_trees.py gpurun_out/ab_c5.jsonl ${C5} $V --steps 20 --no-cpu-baseline --scenario ObstacleAvoidance --agents 12 --envs 512 || exit $?
+fi
 echo "ab ok"
