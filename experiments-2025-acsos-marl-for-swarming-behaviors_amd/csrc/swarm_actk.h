@@ -58,7 +58,7 @@ struct ActSmem {
   // per wave (<= 8 slots): the tick's pair forces [NS][NS][2], formed from the positions the wave
   // loaded while the prologue's optimizer operands are still in flight (they depend on no weight
   // and no action); 16-slot kernels form them after the argmax in the free H rows instead
-  __attribute__((aligned(16))) float FB[kActWPB][NS <= 8 ? 2 * NS * (NS + 1) : 4];
+  __attribute__((aligned(16))) float FB[kActWPB][NS <= 8 ? 2 * NS * (NS + 1) + 2 * NS + 4 * (NS * NS + NS) : 4];
   __attribute__((aligned(16))) float Pw[N_LDS_PARAMS];
   float red[64];   // the optimizer step's norm (adam_norm2_block)
 };
@@ -194,7 +194,19 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // row n of the force matrix at a stride of NS + 1 float2: the force sum's 16 lanes (one agent
   // each) read 16 distinct LDS banks instead of 2 (a stride of 2 NS floats is a multiple of 32)
   constexpr int kFbRow = 2 * (NS + 1);
-  static_assert(3 * NS * kRow >= kFbRow * NS, "pair-force scratch");
+  // then the obstacle pair of every agent (OA) and the list of the tick's pairs in contact
+  constexpr int kFbOb = NS * kFbRow;
+  constexpr int kFbList = kFbOb + 2 * NS;      // [NS * NS + NS][4]: dx, dy, dist, destination
+  // Only where a lane has more than one candidate (16 slots: 4 pair slots; OA: + the obstacle).
+  // GoTo with 8 slots (one pair per lane) and 32 slots (no room for the list) evaluate each pair
+  // in place, as pair_force does: the list only costs there (C2 13.72 -> 13.76 us per tick)
+  constexpr bool kCompact = NS <= 16 && (NS * NS / 64 + (SCEN == SWARM_OBSTACLE_AVOIDANCE ? 1 : 0)) > 1;
+  static_assert(3 * NS * kRow >= (kCompact ? kFbList + 4 * (NS * NS + NS) : kFbOb + 2 * NS), "pair-force scratch");
+  // Every pair's distance and contact test first; pairs out of contact get exactly 0 (the
+  // reference's torch.where); the pairs in contact (and agents touching the obstacle) are then
+  // compacted into a list and evaluated 64 at a time, one per lane, so the transcendental part
+  // runs once per 64 contacts instead of once per pair slot that any lane has in contact (with 16
+  // slots: 4 pair slots + the obstacle per lane).  Same operations per pair as pair_force.
   auto pair_forces = [&]() {
     if (kHoist || MODE == MODE_STEP) {   // else the forward left the positions in sm.px / sm.py
 #pragma unroll
@@ -202,15 +214,58 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
         if (16 * ct + c < NS && p == 0) { sm.px[16 * ct + c] = px[ct]; sm.py[16 * ct + c] = py[ct]; }
       wave_lds_sync();
     }
-    constexpr int LPN = 64 / NS;
+    constexpr int LPN = 64 / NS, NPL = NS / LPN;
     const int n = d.lane / LPN;
     const float pxn = sm.px[n], pyn = sm.py[n];
+    float cdx[NPL + 1], cdy[NPL + 1], cds[NPL + 1];
+    int cof[NPL + 1];
+    bool cin[NPL + 1];
 #pragma unroll
-    for (int j = 0; j < NS / LPN; ++j) {
+    for (int j = 0; j < NPL; ++j) {
       const int u = d.lane % LPN + LPN * j;
-      float gx = 0.0f, gy = 0.0f;
-      if (u < N && n < N) pair_force(pxn - sm.px[u], pyn - sm.py[u], gx, gy);   // u == n: exactly 0
-      *reinterpret_cast<float2*>(fb + n * kFbRow + 2 * u) = make_float2(gx, gy);
+      cdx[j] = pxn - sm.px[u];
+      cdy[j] = pyn - sm.py[u];
+      cds[j] = norm2(cdx[j], cdy[j]);
+      cin[j] = u < N && n < N && pair_contact(cds[j]);   // u == n: distance 0, no contact
+      cof[j] = n * kFbRow + 2 * u;
+      float2 g = make_float2(0.0f, 0.0f);
+      if (!kCompact && cin[j]) contact_force(cdx[j], cdy[j], cds[j], g.x, g.y);
+      if (!kCompact || !cin[j]) *reinterpret_cast<float2*>(fb + cof[j]) = g;
+    }
+    {   // the obstacle pair of agent n, on the agent's first lane
+      const bool lead = d.lane % LPN == 0;
+      cdx[NPL] = pxn - kObstX;
+      cdy[NPL] = pyn - kObstY;
+      cds[NPL] = norm2(cdx[NPL], cdy[NPL]);
+      cin[NPL] = SCEN == SWARM_OBSTACLE_AVOIDANCE && lead && n < N && pair_contact(cds[NPL]);
+      cof[NPL] = kFbOb + 2 * n;
+      float2 g = make_float2(0.0f, 0.0f);
+      if (!kCompact && cin[NPL]) contact_force(cdx[NPL], cdy[NPL], cds[NPL], g.x, g.y);
+      if (SCEN == SWARM_OBSTACLE_AVOIDANCE && lead && (!kCompact || !cin[NPL])) *reinterpret_cast<float2*>(fb + cof[NPL]) = g;
+    }
+    if constexpr (!kCompact) return;
+    uint32_t total = 0;
+#pragma unroll
+    for (int j = 0; j <= NPL; ++j) {
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(cin[j]);
+      if (cin[j]) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        *reinterpret_cast<float4*>(fb + kFbList + 4 * (total + below)) =
+            make_float4(cdx[j], cdy[j], cds[j], __int_as_float(cof[j]));
+      }
+      total += (uint32_t)__builtin_popcountll(m);
+    }
+    if (total != 0u) {
+      wave_lds_sync();
+      for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+        const uint32_t k = k0 + (uint32_t)d.lane;
+        if (k < total) {
+          const float4 e = *reinterpret_cast<const float4*>(fb + kFbList + 4 * k);
+          float gx, gy;
+          contact_force(e.x, e.y, e.z, gx, gy);
+          *reinterpret_cast<float2*>(fb + __float_as_int(e.w)) = make_float2(gx, gy);
+        }
+      }
     }
   };
   // hoisted for graphs of <= 8 agents (one pair per lane); with 16 slots (4 pairs per lane) the
@@ -339,10 +394,9 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
       const int n = min(16 * ct + c, NS - 1);
       float fx = 0.0f + action_level(action[ct] / 3);
       float fy = 0.0f + action_level(action[ct] % 3);
-      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {
-        float gx, gy;
-        pair_force(px[ct] - kObstX, py[ct] - kObstY, gx, gy);
-        fx = fx + gx; fy = fy + gy;
+      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {   // the obstacle pair (pair_forces)
+        const float2 g = *reinterpret_cast<const float2*>(fb + kFbOb + 2 * n);
+        fx = fx + g.x; fy = fy + g.y;
       }
       // every slot read at once, no per-partner branch: slots u >= N hold +0 and fx, fy
       // (started from +0 or +-1) never become -0, so adding them is exact

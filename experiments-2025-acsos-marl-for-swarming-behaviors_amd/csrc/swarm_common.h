@@ -220,16 +220,22 @@ __device__ inline float logaddexp0(float x) {
 // pair (a, b) with delta = p_a - p_b; force on b is the exact negation.
 // Pairs out of contact (dist > r_a + r_b) or coincident (dist < 1e-6) get exactly 0,
 // as the two torch.where of the reference do, so the transcendental part is skipped.
-__device__ inline void pair_force(float dx, float dy, float& fx, float& fy) {
-  const float dist = norm2(dx, dy);
+// In two pieces so that a wave can test every pair first and evaluate only the pairs in contact
+// (swarm_actk.h pair_forces): the same operations in the same order as one call.
+__device__ inline bool pair_contact(float dist) { return !(dist < kMinDist || dist > kRadius + kRadius); }
+__device__ inline void contact_force(float dx, float dy, float dist, float& fx, float& fy) {
   const float dmin = kRadius + kRadius;
-  fx = 0.0f;
-  fy = 0.0f;
-  if (dist < kMinDist || dist > dmin) return;
   const float pen = logaddexp0((dmin - dist) / kContactMargin) * kContactMargin;
   const float den = dist > 0.0f ? dist : 1e-8f;
   fx = kCollisionForce * dx / den * pen;
   fy = kCollisionForce * dy / den * pen;
+}
+__device__ inline void pair_force(float dx, float dy, float& fx, float& fy) {
+  const float dist = norm2(dx, dy);
+  fx = 0.0f;
+  fy = 0.0f;
+  if (!pair_contact(dist)) return;
+  contact_force(dx, dy, dist, fx, fy);
 }
 
 // discrete action a in 0..8 -> u = (L[a/3], L[a%3]), L = {0, -1, +1}  

@@ -11,4 +11,7 @@ fi
 if [ -n "$C5" ]; then
 timeout -k 10 1000 python -u tools/ab_trees.py gpurun_out/ab_c5.jsonl ${C5} $V --steps 20 --no-cpu-baseline --scenario ObstacleAvoidance --agents 12 --envs 512 || exit $?
 fi
+if [ -n "$C5N5" ]; then
+timeout -k 10 1000 python -u tools/ab_trees.py gpurun_out/ab_c5n5.jsonl ${C5N5} $V --steps 20 --no-cpu-baseline --scenario ObstacleAvoidance --agents 5 --envs 512 || exit $?
+fi
 echo "ab ok"
