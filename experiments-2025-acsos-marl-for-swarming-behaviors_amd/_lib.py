@@ -90,7 +90,7 @@ _PROTOS = {
     "swarm_train_act_step": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
                                        POINTER(SwarmReplay), c_void_p, POINTER(SwarmActOut), c_void_p, c_void_p]),
     "swarm_reduce_advance": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p, POINTER(SwarmLearner),
-                                       c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                       c_int32, c_void_p, c_void_p]),
     "swarm_sample_prepare": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_int32, c_void_p, c_void_p,
                                        c_void_p]),
     "swarm_adam_flush": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), POINTER(SwarmLearner), c_void_p,
@@ -118,8 +118,7 @@ _PROTOS = {
     "swarm_peer_ipc_open": (c_int32, [c_void_p, POINTER(c_void_p)]),
     "swarm_peer_ipc_close": (c_int32, [c_void_p]),
     "swarm_reduce_advance_peer": (c_int32, [POINTER(SwarmConfig), POINTER(SwarmAdamCfg), c_void_p,
-                                            POINTER(SwarmLearner), c_int32, c_void_p, c_void_p, c_void_p,
-                                            POINTER(SwarmPeer), c_void_p]),
+                                            POINTER(SwarmLearner), c_int32, c_void_p, POINTER(SwarmPeer), c_void_p]),
     "swarm_peer_allreduce": (c_int32, [POINTER(SwarmPeer), c_void_p, c_int32, c_void_p]),
     "swarm_host_sample_index": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
     "swarm_host_sample_position": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),

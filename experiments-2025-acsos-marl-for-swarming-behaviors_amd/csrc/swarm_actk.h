@@ -38,7 +38,6 @@ struct ActArgs {
   float* grad_norm_out;    // &ctrl->grad_norm (written by block 0)
   int32_t* sample_out;     // MODE_TICK: this tick's TD batch indices [hp.batch] (or NULL)
   unsigned long long* ho_rec;   // fused tick: [B][ho_stride_granules(N)] hand-off records (swarm_common.h)
-  float* state_out;        // fused tick: the stepped states go here (tick workspace), not to `state`
 };
 
 constexpr int kActWPB = 4;   // waves (= environments) per act block; the block is one Adam workgroup
@@ -152,9 +151,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // fused tick: is this env's transition in the TD batch drawn from this tick's slot?
   // (position of graph id slot * B + env in the keyed permutation < batch)
   bool ho_pub = false;
-  // (GoTo / ObstacleAvoidance: the TD blocks recompute the transition from `state`, swarm_tdk.h;
-  // only Flocking's reward state keeps the tagged-granule hand-off)
-  if (MODE == MODE_TICK && HO && SCEN == SWARM_FLOCKING && d.live) {
+  if (MODE == MODE_TICK && HO && d.live) {
     const uint32_t cap = (uint32_t)A.replay.capacity;
     const uint32_t filled = cc.filled_slots;
     const uint32_t ng = (filled + 1 < cap ? filled + 1 : cap) * (uint32_t)B;
@@ -538,13 +535,11 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     }
 #endif
   }
-  // fused tick: into the workspace (swarm_reduce_advance copies it to `state` after the launch)
-  float* st_out = (MODE == MODE_TICK && HO && A.state_out) ? A.state_out : state;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     if (valid[ct] && p == 0) {
-      reinterpret_cast<float4*>(st_out)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
-      if (fl_prev) st_out[(size_t)B * N * 4 + node[ct]] = spread[ct];
+      reinterpret_cast<float4*>(state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
+      if (fl_prev) fl_prev[node[ct]] = spread[ct];
       if (MODE == MODE_ROLLOUT) {
         if (A.out.reward) A.out.reward[node[ct]] = rew_sum[ct];
         if (A.out.obs) {

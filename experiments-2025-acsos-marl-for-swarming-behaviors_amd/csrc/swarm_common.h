@@ -187,16 +187,6 @@ __host__ __device__ inline size_t slab_index(int q, int b, int n_slabs) {
 // Record of env e (granule index): s [N][4] at 4n + k, s' [N][4] at 4N + 4n + k, r at 8N + n,
 // a at 9N + n.
 __host__ __device__ constexpr int ho_stride_granules(int N) { return ((10 * N + 15) / 16) * 16; }
-// Fused-tick workspace: [error word, 512 B][B hand-off records][the tick's stepped states]: the
-// acting blocks write each env's state after the step there (swarm_state_floats layout), so that
-// `state` keeps the states the tick started from for the whole launch (the TD blocks read them),
-// and swarm_reduce_advance copies them to `state`.
-__host__ __device__ constexpr size_t tick_ws_state_offset(int B, int N) {
-  return 512 + (size_t)B * ho_stride_granules(N) * 8;
-}
-__host__ __device__ constexpr size_t state_floats_of(int B, int N, int scenario) {
-  return (size_t)B * N * (scenario == SWARM_FLOCKING ? 5 : 4);
-}
 __device__ inline void st_granule(unsigned long long* g, uint32_t tag, uint32_t value) {
   __hip_atomic_store(g, ((unsigned long long)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -29,19 +29,6 @@ __device__ inline float row4_sum(float x) {
   return __int_as_float((int)b[0]) + __int_as_float((int)b[1]);
 }
 
-// the value of each of the four row groups (lanes l, l^16, l^32, l^48) in every lane: out[q] =
-// row group q's x (permlane16_swap pairs rows 0/1 and 2/3, permlane32_swap the two halves)
-__device__ inline void row4_gather(float x, float out[4]) {
-  const int xi = __float_as_int(x);
-  const auto a = __builtin_amdgcn_permlane16_swap(xi, xi, false, false);   // (even row's, odd row's)
-  const auto e = __builtin_amdgcn_permlane32_swap((int)a[0], (int)a[0], false, false);   // rows 0, 2
-  const auto o = __builtin_amdgcn_permlane32_swap((int)a[1], (int)a[1], false, false);   // rows 1, 3
-  out[0] = __int_as_float((int)e[0]);
-  out[1] = __int_as_float((int)o[0]);
-  out[2] = __int_as_float((int)e[1]);
-  out[3] = __int_as_float((int)o[1]);
-}
-
 // pick v[4 k + p] for this lane's row group p (register arrays cannot be indexed by lane)
 template <int M>
 __device__ inline float pick4(const float (&v)[M], int k, int p) {

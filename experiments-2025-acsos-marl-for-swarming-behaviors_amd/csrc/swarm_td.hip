@@ -6,8 +6,6 @@
 // GraphReplayBuffer.sample (:38-45), Adam(lr=1e-3) (:85), target sync (:131-133).
 #include <stdlib.h>
 
-#include <algorithm>
-
 #include "swarm_tdk.h"
 #include "swarm_peer.h"
 
@@ -39,10 +37,6 @@ struct ReduceArgs {
   swarm_adam_cfg hp;
   uint32_t k0, k1;        // replay-sampling key (seed ^ rank salt)
   swarm_peer peer;        // PEER = 1: the all-reduce over the ranks' exchange buffers (swarm_peer.h)
-  const float* state_src; // fused tick: the stepped states in the tick workspace -> state_dst
-  float* state_dst;
-  int state_n;            // floats to copy (0: none)
-  int state_blocks;       // copy blocks after the w / m / v ones
 };
 
 // 1024 threads = 16 columns x 64 slab groups (105 column blocks: the 1.7 MB of freshly
@@ -145,16 +139,6 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
   swarm_ctrl* C = ctrl;
   if ((int)blockIdx.x > kRedColBlocks) {   // advance mode: a copy-back block
     const int j = (int)blockIdx.x - kRedColBlocks - 1;
-    if (j >= kRedCopyBlocks) {   // the fused tick's stepped states -> state (grid-stride over the copy blocks)
-      const int nt = (int)blockDim.x * A.state_blocks;
-      const int n4 = A.state_n / 4;
-      const float4* src = reinterpret_cast<const float4*>(A.state_src);
-      float4* dst = reinterpret_cast<float4*>(A.state_dst);
-      for (int i = (j - kRedCopyBlocks) * (int)blockDim.x + (int)threadIdx.x; i < n4; i += nt) dst[i] = src[i];
-      if (j == kRedCopyBlocks && (int)threadIdx.x < A.state_n - 4 * n4)
-        A.state_dst[4 * n4 + threadIdx.x] = A.state_src[4 * n4 + threadIdx.x];
-      return;
-    }
     const float4* src = reinterpret_cast<const float4*>(j == 0 ? A.lr.w_nxt : (j == 1 ? A.lr.m_nxt : A.lr.v_nxt));
     float4* dst = reinterpret_cast<float4*>(j == 0 ? A.lr.w_cur : (j == 1 ? A.lr.m_cur : A.lr.v_cur));
     if ((int)threadIdx.x < N_PARAMS_PAD / 4) dst[threadIdx.x] = src[threadIdx.x];
@@ -411,21 +395,11 @@ int swarm_grad_reduce(const swarm_config* cfg, const swarm_adam_cfg* hp, const f
 }
 
 static int reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
-                          int32_t replay_capacity, swarm_ctrl* ctrl, const void* tick_ws, float* state,
-                          const swarm_peer* peer, void* stream) {
+                          int32_t replay_capacity, swarm_ctrl* ctrl, const swarm_peer* peer, void* stream) {
   if (int e = check_td(cfg, hp)) return e;
-  if (!lr || !ctrl || replay_capacity < 1 || (tick_ws == nullptr) != (state == nullptr)) return SWARM_E_BADARG;
+  if (!lr || !ctrl || replay_capacity < 1) return SWARM_E_BADARG;
   ReduceArgs a = {};
   if (peer) a.peer = *peer;
-  if (tick_ws) {   // after swarm_train_tick: its stepped states -> state
-    a.state_src = reinterpret_cast<const float*>(static_cast<const char*>(tick_ws) +
-                                                 tick_ws_state_offset(cfg->n_envs, cfg->n_agents));
-    a.state_dst = state;
-    a.state_n = (int)state_floats_of(cfg->n_envs, cfg->n_agents, cfg->scenario);
-    const int per_block = 4 * kRedCols * kRedGroups;   // floats one block copies per pass
-    a.state_blocks = std::min(64, (a.state_n + per_block - 1) / per_block);
-  }
-  const int grid = kRedColBlocks + 1 + kRedCopyBlocks + a.state_blocks;
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = lr->grad;
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
@@ -433,26 +407,25 @@ static int reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, con
   a.k0 = (uint32_t)(cfg->seed & 0xFFFFFFFFu) ^ ((uint32_t)cfg->env_offset * 0x9E3779B9u);
   a.k1 = (uint32_t)(cfg->seed >> 32);
   if (peer)
-    hipLaunchKernelGGL(grad_reduce_kernel<1>, dim3(grid), dim3(kRedCols * kRedGroups), 0,
+    hipLaunchKernelGGL(grad_reduce_kernel<1>, dim3(kRedColBlocks + 1 + kRedCopyBlocks), dim3(kRedCols * kRedGroups), 0,
                        (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   else
-    hipLaunchKernelGGL(grad_reduce_kernel<0>, dim3(grid), dim3(kRedCols * kRedGroups), 0,
+    hipLaunchKernelGGL(grad_reduce_kernel<0>, dim3(kRedColBlocks + 1 + kRedCopyBlocks), dim3(kRedCols * kRedGroups), 0,
                        (hipStream_t)stream, a.slabs, a.ctrl, a.n_slabs, a.advance, a);
   return (int)hipGetLastError();
 }
 
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs, const swarm_learner* lr,
-                         int32_t replay_capacity, swarm_ctrl* ctrl, const void* tick_workspace, float* state,
-                         void* stream) {
-  return reduce_advance(cfg, hp, slabs, lr, replay_capacity, ctrl, tick_workspace, state, nullptr, stream);
+                         int32_t replay_capacity, swarm_ctrl* ctrl, void* stream) {
+  return reduce_advance(cfg, hp, slabs, lr, replay_capacity, ctrl, nullptr, stream);
 }
 
 int swarm_reduce_advance_peer(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
                               const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
-                              const void* tick_workspace, float* state, const swarm_peer* peer, void* stream) {
+                              const swarm_peer* peer, void* stream) {
   if (int e = check_peer(peer)) return e;
   if (hp && hp->world_size != peer->world_size) return SWARM_E_BADARG;
-  return reduce_advance(cfg, hp, slabs, lr, replay_capacity, ctrl, tick_workspace, state, peer, stream);
+  return reduce_advance(cfg, hp, slabs, lr, replay_capacity, ctrl, peer, stream);
 }
 
 static int launch_adam(const swarm_config* cfg, const swarm_adam_cfg* hp, float* params, float* target, float* m,

@@ -18,7 +18,6 @@
 #pragma once
 #include "swarm_adam.h"
 #include "swarm_dl.h"
-#include "swarm_env.h"
 
 namespace swarm {
 
@@ -54,7 +53,6 @@ struct TdLds {
   int act[kTdRows];
   int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
   int prew[GPB];                  // online wave w is on the pre path (swarm_tdk.h td_body)
-  int rcf[GPB];                   // fused tick: online wave w has put its graphs' s' in X (for target wave w)
   int insl[GPB];                  // before B0: online wave w holds a graph of this tick's slot
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
   __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
@@ -74,7 +72,6 @@ struct TdArgs {
   float gamma;
   float grad_scale;   // fp32(2 / M_local)
   int n_slabs;        // TD blocks of the launch (slab layout, swarm_common.h slab_index)
-  const float* state; // fused tick: the env states the tick starts from ([B][N][4], stable in the launch)
 };
 
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
@@ -152,11 +149,7 @@ __device__ inline void drop_overrun(const bool (&okc)[DGeom<NS>::CT], bool (&dro
     if (bad[ct]) { drop[ct] = true; nv[ct] = false; }
 }
 
-// SPEC: graph + conv fixed at compile time (swarm_common.h).  SCEN: the fused tick's scenario;
-// GoTo / ObstacleAvoidance take the graphs of this tick's own replay slot from `state` and
-// recompute their transition (kRC below); Flocking (and SCEN = -1) reads the acting waves'
-// tagged-granule hand-off records
-template <int NS, int GS, int SPEC, bool FUSED = false, int SCEN = -1>
+template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
                                         const float* rs_next, const float* rr, const uint8_t* ra, int S, int B,
                                         int N, int capacity, const TdArgs& A, const TdFused& X,
@@ -165,16 +158,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
                                         const float* v_pre = nullptr) {
   constexpr int GPB = kTdRows / NS, CT = DGeom<NS>::CT;   // GPB: online (= target) waves per block
   constexpr int GPW = NS / GS;                             // graphs per wave
-  // Recompute the tick's own transitions (fused tick, GoTo / OA): a graph drawn from the replay
-  // slot this tick writes is the env's transition of this very tick.  Its online wave reads s from
-  // `state` (the acting blocks write the stepped states to the workspace, so `state` holds s for
-  // the whole launch), runs its forward at once, takes the env's action as the acting wave does
-  // (the same Philox coin and draws, argmax of the same Q), steps the env with the same fp32
-  // operations (pair forces, force sum in VMAS order, integrator, reward) and hands s' to its target
-  // wave through LDS: no wait on the acting wave, no global hand-off.  Bit-identical to the
-  // replay's (s, a, r, s') that the acting wave pushes (tests: the fused tick == the 3-launch tick).
-  constexpr bool kRC = FUSED && (SCEN == SWARM_GOTO || SCEN == SWARM_OBSTACLE_AVOIDANCE);
-  static_assert(!kRC || (NS == 16 && CT == 1 && GS % 4 == 0), "recompute layout");
   constexpr int NT = 128 * GPB;
   static_assert(!FUSED || NT == kAdamNT, "the fused TD block is one Adam workgroup");
   static_assert(GPB <= 2, "B2 jobs 2 and 3 go to the pre-path online waves by wave index (GPB <= 2)");
@@ -282,8 +265,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       st[ct] = reinterpret_cast<const float4*>(online ? rs : rs_next)[ri];
       rew[ct] = rr[ri];
       act[ct] = nv[ct] ? (int)ra[ri] : 0;
-    } else if (kRC && online) {   // this tick's s: the state the tick started from
-      st[ct] = reinterpret_cast<const float4*>(A.state)[(size_t)genv * N + min(jl[ct], N - 1)];
     }
   }
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
@@ -332,7 +313,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     for (int ct = 0; ct < CT; ++ct)
       if (16 * ct + c < NS) TB.tdrop[row0 + 16 * ct + c] = 0;
   }
-  if (kRC && !online && lane == 0) TB.rcf[wi] = 0;   // set by online wave wi once s' is in X
   __syncthreads();   // B0: weight images
   SWARM_STAMP(2);
   bool pre = false;
@@ -344,26 +324,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   auto ho_at = [&](int ct, int off, int per_node) -> const unsigned long long* {
     return ho_rec + (size_t)(gid[ct] % (uint32_t)B) * ho_stride_granules(N) + off + per_node * min(jl[ct], N - 1);
   };
-  if (kRC && waited && !online) {   // s' of the recomputed transitions, from the online wave (LDS)
-    for (int spin = 0;; ++spin) {
-      if (*(volatile int*)&TB.rcf[wi] != 0) break;
-      if (spin >= kHoSpinLimit) {   // never: the online wave has no wait before it sets the flag
-        if (lane == 0) atomicAdd(X.ho_err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-      if (ho[ct]) {
-        const int row = row0 + min(16 * ct + c, NS - 1);
-        st[ct] = make_float4(TB.X[row][0], TB.X[row][1], TB.X[row][2], TB.X[row][3]);
-      }
-    __builtin_amdgcn_s_setprio(3);   // waves of this tick's graphs are the tick's critical path
-  }
-  if (waited && kRC && online) __builtin_amdgcn_s_setprio(3);
-  if (waited && !kRC) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off): online
+  if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off): online
                   // waves s (published at the acting prologue), target waves s' (after the integrator).
                   // Wave-local, after B0: the block's other waves are not held by it
     for (int spin = 0;; ++spin) {
@@ -417,72 +378,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // fused: the rest of this tick's transitions, each as late as its first use: a for the online
   // waves' pre path here; r (published after the acting wave's reward) by the online waves after
   // it, in their wait for the target waves' y, so no poll sits between the target forward and B1
-  if (kRC && waited && online) {   // the transition of this tick's graphs, as the acting wave forms it
-    WSmall<NS>& sm = *V.sm;        // sm.px / sm.py: this wave's slot positions (dl_forward)
-    constexpr int PPL = GS / 4;    // partners per lane: u = p + 4 j of the lane's node
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int n = min(16 * ct + c, NS - 1);
-      const int base = (GS < NS) ? (n / GS) * GS : 0;
-      const int jn = jl[ct];
-      const uint32_t genv = (uint32_t)A.env_offset + gid[ct] % (uint32_t)B;
-      // eps-greedy (act_body; train_gcn_dqn.py:164-168): the env's coin, its random draws, argmax
-      int a = argmax9(F.q[ct]);
-      if (cc.eps > 0.0f && u01(philox4x32(cc.tick, genv, STREAM_COIN, 0u, A.k0, A.k1).x) < cc.eps) {
-        const int agent = min(jn, N - 1);
-        const u32x4 wd = philox4x32(cc.tick, genv, STREAM_RAND_ACTION, (uint32_t)(agent >> 2), A.k0, A.k1);
-        const int j = agent & 3;
-        a = uniform_int(j == 0 ? wd.x : (j == 1 ? wd.y : (j == 2 ? wd.z : wd.w)), kActions);
-      }
-      // VMAS pair forces of node n's graph: this lane's partners, then all GS in every row group
-      const float pxn = sm.px[n], pyn = sm.py[n];
-      float fpx[GS], fpy[GS];
-#pragma unroll
-      for (int j = 0; j < PPL; ++j) {
-        const int u = p + 4 * j;
-        float gx = 0.0f, gy = 0.0f;
-        if (u < N && jn < N) pair_force(pxn - sm.px[base + u], pyn - sm.py[base + u], gx, gy);
-        float ox[4], oy[4];
-        row4_gather(gx, ox);
-        row4_gather(gy, oy);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { fpx[4 * j + q] = ox[q]; fpy[4 * j + q] = oy[q]; }
-      }
-      // force sum in VMAS order: 0 + u, the obstacle pair, agent pairs in ascending partner index
-      float fx = 0.0f + action_level(a / 3);
-      float fy = 0.0f + action_level(a % 3);
-      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {
-        float gx, gy;
-        pair_force(pxn - kObstX, pyn - kObstY, gx, gy);
-        fx = fx + gx; fy = fy + gy;
-      }
-#pragma unroll
-      for (int u = 0; u < GS; ++u) { fx = fx + fpx[u]; fy = fy + fpy[u]; }
-      const StepOut o = integrate(st[ct].x, st[ct].y, st[ct].z, st[ct].w, fx, fy);
-      if (16 * ct + c < NS && p == 0) sm.aux[16 * ct + c] = o.dgoal;   // sm.aux: free after the forward
-      wave_lds_sync();
-      float r;
-      if (SCEN == SWARM_GOTO) {   // go_to_position_scenario.py:112-113: - sum of every agent's distance
-        float dj[GS];
-#pragma unroll
-        for (int j = 0; j < GS; ++j) dj[j] = sm.aux[base + (j < N ? j : 0)];
-        r = -dj[0];
-#pragma unroll
-        for (int j = 1; j < GS; ++j)
-          if (j < N) r = r + (-dj[j]);
-      } else {
-        r = oa_reward(o.dgoal, o.dobs);
-      }
-      if (ho[ct]) { act[ct] = nv[ct] ? a : 0; rew[ct] = r; }
-      if (16 * ct + c < NS) {   // s' for the target wave: component p of node n (X is free until B1)
-        TB.X[row0 + 16 * ct + c][p] = p == 0 ? o.px : (p == 1 ? o.py : (p == 2 ? o.vx : o.vy));
-        if (p == 0) TB.act[row0 + 16 * ct + c] = nv[ct] ? act[ct] : 0;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) *(volatile int*)&TB.rcf[wi] = 1;
-  }
-  if (FUSED && !kRC && waited && online) {
+  if (FUSED && waited && online) {
     for (int spin = 0;; ++spin) {
       bool ok = true, okc[CT];
 #pragma unroll
@@ -605,7 +501,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
   }
-  if (FUSED && !kRC && waited && online) {   // r of this tick's transitions (y = r + gamma max Q_tgt after B1)
+  if (FUSED && waited && online) {   // r of this tick's transitions (y = r + gamma max Q_tgt after B1)
     for (int spin = 0;; ++spin) {
       bool ok = true, okc[CT];
 #pragma unroll

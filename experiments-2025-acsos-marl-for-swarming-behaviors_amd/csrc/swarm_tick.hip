@@ -43,9 +43,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2
     act_body<NSA, MODE_TICK, SCEN, SPEC, true, SWARM_NET_GCN>(U.a, blockIdx.x, n_act, ctrl, state, grad, w_cur, m_cur,
                                                               v_cur, B, N, A);
   } else {
-    td_body<NST, GS, SPEC, true, SCEN>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next,
-                                            T.replay.r, T.replay.a, T.S, B, N, T.replay.capacity, T, X, ctrl, grad,
-                                            w_cur, m_cur, v_cur);
+    td_body<NST, GS, SPEC, true>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next, T.replay.r,
+                                      T.replay.a, T.S, B, N, T.replay.capacity, T, X, ctrl, grad, w_cur, m_cur, v_cur);
   }
 }
 
@@ -54,11 +53,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2
 using namespace swarm;
 
 namespace {
-// workspace: [err: 1 u32, padded to 512 B], the tagged hand-off records, the stepped states
-// (swarm_common.h tick_ws_state_offset)
+// workspace: [err: 1 u32, padded to 512 B], then the tagged hand-off records
 size_t err_bytes() { return 512; }
 size_t rec_bytes(int B, int N) { return (size_t)B * ho_stride_granules(N) * 8; }
-static_assert(tick_ws_state_offset(3, 5) == 512 + 3 * ho_stride_granules(5) * 8, "workspace layout");
 }  // namespace
 
 extern "C" {
@@ -75,8 +72,7 @@ int swarm_train_tick_supported(const swarm_config* cfg) {
 
 int64_t swarm_train_tick_workspace_bytes(const swarm_config* cfg) {
   if (!swarm_train_tick_supported(cfg)) return SWARM_E_UNSUPPORTED;
-  return (int64_t)(tick_ws_state_offset(cfg->n_envs, cfg->n_agents) +
-                   4 * state_floats_of(cfg->n_envs, cfg->n_agents, cfg->scenario));
+  return (int64_t)(err_bytes() + rec_bytes(cfg->n_envs, cfg->n_agents));
 }
 
 int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const swarm_learner* lr, float* state,
@@ -100,14 +96,12 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   a.replay = *replay;
   if (out) a.out = *out;
   a.ho_rec = rec;
-  a.state_out = reinterpret_cast<float*>(ws + tick_ws_state_offset(B, N));
 
   TdArgs t = {};
   t.S = hp->batch; t.B = B; t.N = N; t.graph = cfg->graph; t.k = cfg->knn_k; t.conv = cfg->conv;
   t.env_offset = cfg->env_offset; t.k0 = a.k0; t.k1 = a.k1; t.radius = cfg->radius;
   t.params = lr->w_nxt; t.target = lr->target; t.replay = *replay; t.ctrl = ctrl;
   t.sample_in = nullptr; t.sample_out = sample_out; t.slabs = slabs;
-  t.state = state;   // the states the tick starts from (stable during the launch: acting writes state_out)
   t.gamma = hp->gamma;
   t.grad_scale = (float)(2.0 / ((double)hp->batch * (double)N));
 

@@ -324,21 +324,17 @@ class SwarmEngine:
                                         ctypes_ref(self.out if full_out else self.out_min), ptr(self.slabs),
                                         ptr(self.tick_ws), ptr(self.samples), stream_ptr()), "swarm_train_tick")
 
-    def launch_reduce_advance(self, fused: bool = True):
-        """Slab reduce + ctrl advance; with a peer exchange, the gradient all-reduce too.  After the
-        fused tick it also copies the tick's stepped environments from the workspace to `state`
-        (fused=False: after swarm_train_act_step, which wrote `state` itself)."""
-        ws, st = (ptr(self.tick_ws), ptr(self._state_buf)) if fused and self.tick_ws is not None else (None, None)
+    def launch_reduce_advance(self):
+        """Slab reduce + ctrl advance; with a peer exchange, the gradient all-reduce too."""
         if self.peer is not None:
             self.peer.check_stream()
             check(self.lib.swarm_reduce_advance_peer(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
-                                                     ctypes_ref(self.learner), self.capacity, ptr(self.ctrl), ws, st,
+                                                     ctypes_ref(self.learner), self.capacity, ptr(self.ctrl),
                                                      ctypes_ref(self.peer.struct), stream_ptr()),
                   "swarm_reduce_advance_peer")
             return
         check(self.lib.swarm_reduce_advance(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
-                                            ctypes_ref(self.learner), self.capacity, ptr(self.ctrl), ws, st,
-                                            stream_ptr()),
+                                            ctypes_ref(self.learner), self.capacity, ptr(self.ctrl), stream_ptr()),
               "swarm_reduce_advance")
 
     def handoff_errors(self) -> int:
@@ -379,7 +375,7 @@ class SwarmEngine:
         check(self.lib.swarm_td_grad(cfg, hp, ptr(self.w_nxt), ptr(self.target), ctypes_ref(self.replay),
                                      ptr(self.ctrl), ptr(self.samples), None, ptr(self.slabs), stream_ptr()),
               "swarm_td_grad")
-        self.launch_reduce_advance(fused=False)
+        self.launch_reduce_advance()
         if self.peer is None:
             self.allreduce_grad()
 

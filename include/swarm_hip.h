@@ -257,13 +257,9 @@ uint32_t swarm_host_sample_index(uint32_t i, uint32_t n, uint32_t k0, uint32_t k
 uint32_t swarm_host_sample_position(uint32_t g, uint32_t n, uint32_t k0, uint32_t k1, uint32_t tick);
 
 /* Slab sum -> lr->grad, copy *_nxt -> *_cur, record the pending update and
- * advance ctrl (tick, replay slot, the next step's Adam scalars).  After swarm_train_tick pass
- * its workspace and state (ABI 10): the fused tick leaves the stepped environments in the
- * workspace (the TD blocks read the tick's own states from `state` meanwhile) and this launch
- * copies them to `state`; after swarm_train_act_step (3-launch tick) pass NULL, NULL. */
+ * advance ctrl (tick, replay slot, the next step's Adam scalars). */
 int swarm_reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
-                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
-                         const void* tick_workspace, float* state, void* stream);
+                         const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl, void* stream);
 
 /* ---- Peer all-reduce over xGMI (the one exchange of the data-parallel tick).
  * The reference has no distributed code; this replaces the RCCL all_reduce(grad) that would
@@ -307,8 +303,7 @@ int swarm_peer_ipc_close(void* buf);
  * (ctrl->loss stays this rank's own loss, as with swarm_reduce_advance + RCCL). */
 int swarm_reduce_advance_peer(const swarm_config* cfg, const swarm_adam_cfg* hp, const float* slabs,
                               const swarm_learner* lr, int32_t replay_capacity, swarm_ctrl* ctrl,
-                              const void* tick_workspace, float* state, const swarm_peer* peer,
-                              void* stream);
+                              const swarm_peer* peer, void* stream);
 
 /* Standalone in-place SUM all-reduce of x[n] (n <= N_PARAMS + 1) over the ranks of `peer`
  * (rank-ordered, bitwise identical on every rank); the unfused API path's replacement of

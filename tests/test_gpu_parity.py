@@ -691,9 +691,7 @@ def test_handoff_overrun_drops_the_waiting_graphs(sw, golden_weights):
     lib = _lib.load_variant(build.HODROP_OUT)
     B, N, S, slots = 32, 8, 32, 2
     p = _params(golden_weights, "go_to", 2)
-    # Flocking: the scenario whose fused tick keeps the tagged-granule hand-off (GoTo / OA recompute
-    # the tick's own transitions in the TD blocks and never wait)
-    eng = sw.SwarmEngine("Flocking", N, B, seed=4, params=p, batch=S, eps=0.3, replay_capacity=slots * B,
+    eng = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, batch=S, eps=0.3, replay_capacity=slots * B,
                          update_target_every=1000)
     assert eng.fused
     eng.lib = lib
@@ -732,8 +730,8 @@ def test_handoff_overrun_is_counted_once_per_dropping_wave(sw, golden_weights):
     lib = _lib.load_variant(build.HODROP2_OUT)
     B, N, S, slots = 32, 8, 32, 2
     p = _params(golden_weights, "go_to", 2)
-    eng = sw.SwarmEngine("Flocking", N, B, seed=4, params=p, batch=S, eps=0.3, replay_capacity=slots * B,
-                         update_target_every=1000)   # the granule hand-off scenario (see above)
+    eng = sw.SwarmEngine("GoTo", N, B, seed=4, params=p, batch=S, eps=0.3, replay_capacity=slots * B,
+                         update_target_every=1000)
     assert eng.fused
     eng.lib = lib
     eng.reset(0)

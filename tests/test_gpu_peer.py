@@ -214,7 +214,7 @@ def test_two_rank_peer_tick_equals_hand_made_allreduce(sw, rank_streams, golden_
                 else:
                     e.launch_train_act()
                     e.launch_td()
-                e.launch_reduce_advance(fused=fused)
+                e.launch_reduce_advance()
             g = ha[0].grad + ha[1].grad
             for e in ha:
                 e.grad.copy_(g)
