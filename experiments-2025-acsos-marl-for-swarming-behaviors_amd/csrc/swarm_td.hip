@@ -14,13 +14,13 @@ namespace swarm {
 // One TD block = 32 node slots (swarm_tdk.h).  The dependent chain's pointers (batch indices
 // -> replay rows) and the geometry lead the parameter list: preloaded into SGPRs (kernarg
 // preload), the index loads issue at wave start.
-template <int NS, int GS, int SPEC, int TRA = kTdRows>
+template <int NS, int GS, int SPEC>
 __global__ __launch_bounds__(128 * (kTdRows / NS)) void td_kernel(const int32_t* sample_in, const float* rs,
                                                                   const float* rs_next, const float* rr,
                                                                   const uint8_t* ra, int S, int B, int N,
                                                                   int capacity, TdArgs A) {
   __shared__ TdSmem<NS> L;
-  td_body<NS, GS, SPEC, false, TRA>(L, blockIdx.x, sample_in, rs, rs_next, rr, ra, S, B, N, capacity, A, TdFused{});
+  td_body<NS, GS, SPEC>(L, blockIdx.x, sample_in, rs, rs_next, rr, ra, S, B, N, capacity, A, TdFused{});
 }
 
 // ---------------------------------------------------------------- slab reduction
@@ -318,10 +318,9 @@ using namespace swarm;
 
 namespace {
 int td_slots(int N) { return N <= 8 ? 8 : (N <= 16 ? 16 : 32); }
-// one block per 32 node slots = 32 / GS sampled graphs (thin blocks: 16 node slots, td_thin)
+// one block per 32 node slots = 32 / NS sampled graphs
 int td_blocks(const swarm_config* cfg, int batch) {
-  const int rows = td_thin(cfg->n_envs, cfg->n_agents) ? kThinRows : kTdRows;
-  const int gpb = rows / td_slots(cfg->n_agents);
+  const int gpb = kTdRows / td_slots(cfg->n_agents);
   return (batch + gpb - 1) / gpb;
 }
 int td_max_blocks(const swarm_config* cfg, int batch) { return td_blocks(cfg, batch); }
@@ -364,15 +363,9 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   a.n_slabs = nb;
   hipStream_t st = (hipStream_t)stream;
   const int spec = spec_of(a.graph, a.conv);   // training graphs are complete: GAT and GCN specialised
-  const bool thin = td_thin(cfg->n_envs, cfg->n_agents);
-#define SWARM_TD_LAUNCH2(NS, GS, NT, SP, TRA)                                                                     \
-  hipLaunchKernelGGL((td_kernel<NS, GS, SP, TRA>), dim3(nb), dim3(NT), 0, st, a.sample_in, a.replay.s,              \
-                     a.replay.s_next, a.replay.r, a.replay.a, a.S, a.B, a.N, a.replay.capacity, a)
-#define SWARM_TD_LAUNCH1(NS, GS, NT, SP)                                                                   \
-  do {                                                                                                     \
-    if (NS == 16 && thin) SWARM_TD_LAUNCH2(NS, GS, NT, SP, (NS == 16 ? kThinRows : kTdRows));             \
-    else SWARM_TD_LAUNCH2(NS, GS, NT, SP, kTdRows);                                                        \
-  } while (0)
+#define SWARM_TD_LAUNCH1(NS, GS, NT, SP)                                                                       \
+  hipLaunchKernelGGL((td_kernel<NS, GS, SP>), dim3(nb), dim3(NT), 0, st, a.sample_in, a.replay.s, a.replay.s_next, \
+                     a.replay.r, a.replay.a, a.S, a.B, a.N, a.replay.capacity, a)
 #define SWARM_TD_LAUNCH(NS, GS, NT)                                                       \
   do {                                                                                    \
     if (spec == SPEC_COMPLETE_GAT) SWARM_TD_LAUNCH1(NS, GS, NT, SPEC_COMPLETE_GAT);      \
@@ -384,7 +377,6 @@ int swarm_td_grad(const swarm_config* cfg, const swarm_adam_cfg* hp, const float
   else SWARM_TD_LAUNCH(32, 32, 128);
 #undef SWARM_TD_LAUNCH
 #undef SWARM_TD_LAUNCH1
-#undef SWARM_TD_LAUNCH2
   return (int)hipGetLastError();
 }
 

@@ -28,14 +28,6 @@ namespace swarm {
 // gradient of the block is a sum over its 32 node rows: MFMA 16x16x4 f32 tiles with the
 // node index as K, spread over the waves, each writing its slice of the slab.
 constexpr int kTdRows = 32;
-// Thin TD blocks (TRA = 16 active rows: one online + target wave pair, the other pair idle but at
-// every barrier and sharing the parameter products) for shards of <= kThinEnvs environments, where
-// half the CUs would otherwise idle (C5: 512 envs per GPU): twice the blocks, each product summing
-// 16 node rows instead of 32.  The rule is a function of the configuration only, so the fused,
-// 3-launch and unfused launches group the batch alike and stay bit-identical to each other.
-constexpr int kThinRows = 16;
-constexpr int kThinEnvs = 512;
-__host__ __device__ inline bool td_thin(int n_envs, int n_agents) { return n_agents <= 16 && n_envs <= kThinEnvs; }
 
 template <int NS>
 struct TdLds {
@@ -157,9 +149,7 @@ __device__ inline void drop_overrun(const bool (&okc)[DGeom<NS>::CT], bool (&dro
     if (bad[ct]) { drop[ct] = true; nv[ct] = false; }
 }
 
-// SPEC: graph + conv fixed at compile time (swarm_common.h).  TRA: node rows holding graphs
-// (kTdRows, or kThinRows for thin blocks)
-template <int NS, int GS, int SPEC, bool FUSED = false, int TRA = kTdRows>
+template <int NS, int GS, int SPEC, bool FUSED = false>   // SPEC: graph + conv fixed at compile time (swarm_common.h)
 __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32_t* sample_in, const float* rs,
                                         const float* rs_next, const float* rr, const uint8_t* ra, int S, int B,
                                         int N, int capacity, const TdArgs& A, const TdFused& X,
@@ -177,8 +167,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   const int wave = threadIdx.x >> 6;
   const bool online = wave < GPB;
   const int wi = online ? wave : wave - GPB;
-  static_assert(TRA == kTdRows || (TRA == kThinRows && NS == 16), "thin blocks: one 16-slot wave pair");
-  const bool active = wi < TRA / NS;   // a thin block's second pair holds no graph
   const DGeom<NS> d = make_dgeom<NS>(vb * GPB + wi, 1 << 30);   // lane geometry; liveness is per graph
   const int graph = spec_graph<SPEC>(A.graph);
   const int conv = spec_conv<SPEC>(A.conv);
@@ -229,8 +217,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     const int n = 16 * ct + c;
     const int gi = (GS < NS) ? n / GS : 0;
     jl[ct] = (GS < NS) ? n % GS : n;
-    sid[ct] = vb * (TRA / GS) + wi * GPW + gi;
-    live[ct] = active && sid[ct] < S && n < NS;
+    sid[ct] = vb * (kTdRows / GS) + wi * GPW + gi;
+    live[ct] = sid[ct] < S && n < NS;
     nv[ct] = live[ct] && jl[ct] < N;
     gid[ct] = 0;
     if (!FUSED && sample_in) gid[ct] = min((uint32_t)sample_in[min(sid[ct], S - 1)], ring_graphs - 1u);
@@ -330,7 +318,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   bool pre = false;
 #pragma unroll
   for (int w2 = 0; w2 < GPB; ++w2) pre = pre || TB.insl[w2] != 0;
-  pre = pre && online && active;
+  pre = pre && online;
   const uint32_t tag = cc.tick + 1u;
   // granule address of this lane's node in a hand-off record: s at 0, s' at 4N, r at 8N, a at 9N
   auto ho_at = [&](int ct, int off, int per_node) -> const unsigned long long* {
@@ -386,7 +374,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // ---- forwards: online on s (activations kept), target on s' (train_gcn_dqn.py:119-121).
   //      Everything after B1 waits for the target waves' y, so they issue first.
   if (!online && !waited) __builtin_amdgcn_s_setprio(2);
-  if (active) dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, A.radius, conv, nullptr, V, online, F);
+  dl_forward<NS, 16, GS>(online ? Pon : Ptg, d, N, graph, A.k, A.radius, conv, nullptr, V, online, F);
   // fused: the rest of this tick's transitions, each as late as its first use: a for the online
   // waves' pre path here; r (published after the acting wave's reward) by the online waves after
   // it, in their wait for the target waves' y, so no poll sits between the target forward and B1
@@ -549,7 +537,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  if (!online && p == 0 && active) {
+  if (!online && p == 0) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       float qmax = F.q[ct][0];
@@ -569,7 +557,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 
   const float* P = Pon;
   float dz[CT][2][4];
-  if (online && active) {
+  if (online) {
     // ---- dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ, dZ = dR * [z > 0]
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
@@ -634,11 +622,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   // and an LDS round trip in front of each MFMA): 24 MFMAs of 32 cycles where the 32x32x2 form
   // had 16 of 64 per product, and dW2 takes 16 rows of work instead of 32.
   auto b2_tiles = [&](int tj) {   // lane (c, p) of the D layout: column c, k-slot / row group p
-    constexpr int KS = TRA / 4;   // k-steps: 4 node rows each
-    float a1[2][KS], b1[KS], a2[KS], b2v[KS];
-    int an[KS];
+    float a1[2][8], b1[8], a2[8], b2v[8];
+    int an[8];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+    for (int s = 0; s < 8; ++s) {
       const int n = 4 * s + p;
       a1[0][s] = TB.dZ[n][c];
       a1[1][s] = TB.dZ[n][16 + c];
@@ -648,10 +635,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       a2[s] = TB.gq[n];
     }
 #pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+    for (int s = 0; s < 8; ++s) {
       d0 = mfma16(a1[0][s], b1[s], d0);
       d1 = mfma16(a1[1][s], b1[s], d1);
       d2 = mfma16(an[s] == c ? a2[s] : 0.0f, b2v[s], d2);
@@ -666,12 +653,12 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
     if (job == 2) {
       if (lane < kHidden) {
-        float v[TRA];
+        float v[kTdRows];
 #pragma unroll
-        for (int n = 0; n < TRA; ++n) v[n] = TB.dZ[n][lane];
+        for (int n = 0; n < kTdRows; ++n) v[n] = TB.dZ[n][lane];
         float acc = v[0];
 #pragma unroll
-        for (int n = 1; n < TRA; ++n) acc = acc + v[n];
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
         sst(OFF_B1 + lane, acc);
       }
     } else if (lane < kActions || lane == 63) {   // db2 / loss: the ordered sum over the 32 rows,
@@ -679,7 +666,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       // a branch and an LDS round trip per row)
       float acc = 0.0f;
 #pragma unroll
-      for (int k = 0; k < TRA; k += 8) {
+      for (int k = 0; k < kTdRows; k += 8) {
         int a8[8];
         float g8[8], d8[8];
 #pragma unroll
@@ -697,7 +684,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   };
 
   const int col = lane & 31, h = lane >> 5;
-  if (online && active) {
+  if (online) {
     float da_d[CT];
     WSmall<NS>& sm = *V.sm;
 #pragma unroll
@@ -843,7 +830,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
     SWARM_STAMP(27);
-  } else if (!online) {
+  } else {
     // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
     //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
     //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
@@ -868,36 +855,36 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         const int t = job;
         // operands read up front and unconditionally (column 8 of X is +0: the padding columns
         // c >= kFeat read it), so no LDS round trip sits between two MFMAs of the chain
-        float ha[TRA / 4], xb[TRA / 4];
+        float ha[kTdRows / 4], xb[kTdRows / 4];
 #pragma unroll
-        for (int ks = 0; ks < TRA / 4; ++ks) {
+        for (int ks = 0; ks < kTdRows / 4; ++ks) {
           const int n = 4 * ks + p;
           ha[ks] = TB.dH[n][16 * t + c];
           xb[ks] = TB.X[n][c < kFeat ? c : 8];
         }
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < TRA / 4; ++ks) acc = mfma16(ha[ks], xb[ks], acc);
+        for (int ks = 0; ks < kTdRows / 4; ++ks) acc = mfma16(ha[ks], xb[ks], acc);
         if (c < kFeat) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) sst(OFF_W + (16 * t + 4 * p + r) * kFeat + c, acc[r]);
         }
       } else if (job == 2) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
         const float* da = h == 0 ? TB.das : TB.dad;
-        float v[TRA];
+        float v[kTdRows];
 #pragma unroll
-        for (int n = 0; n < TRA; ++n) v[n] = da[n] * TB.H[n][col];
+        for (int n = 0; n < kTdRows; ++n) v[n] = da[n] * TB.H[n][col];
         float acc = v[0];
 #pragma unroll
-        for (int n = 1; n < TRA; ++n) acc = acc + v[n];
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
         sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, acc);
       } else if (lane < kHidden) {
-        float v[TRA];
+        float v[kTdRows];
 #pragma unroll
-        for (int n = 0; n < TRA; ++n) v[n] = TB.dO[n][lane];
+        for (int n = 0; n < kTdRows; ++n) v[n] = TB.dO[n][lane];
         float acc = v[0];
 #pragma unroll
-        for (int n = 1; n < TRA; ++n) acc = acc + v[n];
+        for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
         sst(OFF_BIAS + lane, acc);
       }
     }

@@ -29,7 +29,7 @@ union TickSmem {
 // CUs), so 2 waves per SIMD is all it needs, and at that target the compiler keeps the MFMA
 // accumulators in ArchVGPRs (no AGPR copies): 15.22 -> 15.07 us per tick (profiles/r02_ab_wpe.jsonl).
 // N > 8 (one graph per TD wave) keeps 3: C3's 768 blocks must all be resident.
-template <int NSA, int NST, int GS, int SCEN, int SPEC, int TRA>
+template <int NSA, int NST, int GS, int SCEN, int SPEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2 : 3, GS == 8 ? 2 : 3))) void tick_kernel(const swarm_ctrl* __restrict__ ctrl, float* state,
                                                    const float* grad, const float* w_cur, const float* m_cur,
                                                    const float* v_cur, int B, int N, ActArgs A,
@@ -43,9 +43,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS == 8 ? 2
     act_body<NSA, MODE_TICK, SCEN, SPEC, true, SWARM_NET_GCN>(U.a, blockIdx.x, n_act, ctrl, state, grad, w_cur, m_cur,
                                                               v_cur, B, N, A);
   } else {
-    td_body<NST, GS, SPEC, true, TRA>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next,
-                                           T.replay.r, T.replay.a, T.S, B, N, T.replay.capacity, T, X, ctrl, grad,
-                                           w_cur, m_cur, v_cur);
+    td_body<NST, GS, SPEC, true>(U.t, (int)blockIdx.x - n_act, nullptr, T.replay.s, T.replay.s_next, T.replay.r,
+                                      T.replay.a, T.S, B, N, T.replay.capacity, T, X, ctrl, grad, w_cur, m_cur, v_cur);
   }
 }
 
@@ -111,9 +110,7 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
 
   const int n_act = (B + kActWPB - 1) / kActWPB;
   const int gs = N <= 8 ? 8 : 16;
-  const bool thin = td_thin(B, N);   // thin TD blocks for small shards (swarm_tdk.h)
-  const int rows = thin ? kThinRows : kTdRows;
-  const int n_td = (hp->batch + (rows / gs) - 1) / (rows / gs);
+  const int n_td = (hp->batch + (kTdRows / gs) - 1) / (kTdRows / gs);
   t.n_slabs = n_td;
   const dim3 grid(n_act + n_td), block(256);
   hipStream_t st = (hipStream_t)stream;
@@ -123,15 +120,8 @@ int swarm_train_tick(const swarm_config* cfg, const swarm_adam_cfg* hp, const sw
   // north_star graph, N <= 8): graph and conv fixed at compile time; others: the
   // runtime-switched kernel
   const int spec = spec_of(cfg->graph, cfg->conv);
-#define SWARM_TICK_LAUNCH(NSA, GS, SC, SP)                                                                        \
-  do {                                                                                                            \
-    if (thin)                                                                                                     \
-      hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP, kThinRows>), grid, block, 0, st, ctrl, state, g, w, m, v, \
-                         B, N, a, t, x);                                                                          \
-    else                                                                                                          \
-      hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP, kTdRows>), grid, block, 0, st, ctrl, state, g, w, m, v, \
-                         B, N, a, t, x);                                                                          \
-  } while (0)
+#define SWARM_TICK_LAUNCH(NSA, GS, SC, SP)                                                                      \
+  hipLaunchKernelGGL((tick_kernel<NSA, 16, GS, SC, SP>), grid, block, 0, st, ctrl, state, g, w, m, v, B, N, a, t, x)
 #define SWARM_TICK_LAUNCH2(NSA, GS, SC)                                               \
   do {                                                                                 \
     if (spec == SPEC_COMPLETE_GAT) SWARM_TICK_LAUNCH(NSA, GS, SC, SPEC_COMPLETE_GAT);  \
