@@ -42,27 +42,20 @@ struct TdLds {
   float dO[kTdRows][kRow];        // dL/d conv out
   float dH[kTdRows][kRow];        // dL/d h
   float X[kTdRows][9];            // node features (k < 8)
-  // per wave pair w: the cm / dp rows of its NS node rows, before B1 target wave w's small
-  // scratch.  Per pair, so that a split block's early online wave can write its cm / dp rows
-  // while the other pair's target wave still runs its forward
-  union PairScratch {
+  union {
     struct {
-      float cm[NS][NS + 1];       // c[target row][source slot]
-      float dp[NS][NS + 1];       // dL/d pre-activation of edge (source -> target row)
+      float cm[kTdRows][NS + 1];  // c[target row][source slot]
+      float dp[kTdRows][NS + 1];  // dL/d pre-activation of edge (source -> target row)
     };
-    WSmall<NS> tgsm;
+    WSmall<NS> tgsm[GPB];         // before B1: the target waves' small scratch
   };
-  PairScratch ps[GPB];
   float yq[kTdRows], gq[kTdRows], das[kTdRows], dad[kTdRows], d2[kTdRows];   // yq: gamma max_a Q_target(s')
   int act[kTdRows];
   int tdrop[kTdRows];             // fused tick: the target wave dropped this row's graph (hand-off overrun)
   int prew[GPB];                  // online wave w is on the pre path (swarm_tdk.h td_body)
   int insl[GPB];                  // before B0: online wave w holds a graph of this tick's slot
-  int fl[4];                      // split blocks: the early pair's LDS flags (y, images, dH)
   WSmall<NS> on[GPB];             // online waves' per-graph scratch
-  __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &ps[w].tgsm}; }
-  __device__ float* cm_row(int row) { return ps[row / NS].cm[row % NS]; }
-  __device__ float* dp_row(int row) { return ps[row / NS].dp[row % NS]; }
+  __device__ WView<NS> target_view(int w) { return WView<NS>{dZ + NS * w, dO + NS * w, dH + NS * w, &tgsm[w]}; }
 };
 
 struct TdArgs {
@@ -111,9 +104,6 @@ struct TdFused {
 #endif
 #ifndef SWARM_HO_FORCE_DROP
 #define SWARM_HO_FORCE_DROP 0
-#endif
-#ifndef SWARM_TD_SPLIT
-#define SWARM_TD_SPLIT 1   // split blocks (td_body); 0: every block in the plain row order, one pass
 #endif
 #ifndef SWARM_HO_SLEEP
 #define SWARM_HO_SLEEP 1  // s_sleep argument (x 64 cycles) between two hand-off sweeps
@@ -323,28 +313,12 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     for (int ct = 0; ct < CT; ++ct)
       if (16 * ct + c < NS) TB.tdrop[row0 + 16 * ct + c] = 0;
   }
-  if (threadIdx.x < 4) TB.fl[threadIdx.x] = 0;
   __syncthreads();   // B0: weight images
   SWARM_STAMP(2);
   bool pre = false;
 #pragma unroll
   for (int w2 = 0; w2 < GPB; ++w2) pre = pre || TB.insl[w2] != 0;
   pre = pre && online;
-  // Split blocks (GPB = 2, exactly one wave pair E' holding graphs of this tick's slot): every
-  // row sum of the block's gradient runs in the K order "the other pair's rows first" (row
-  // k ^ sw), so the early pair E's whole share (its y, images, dH, and the first half of every
-  // MFMA chain and ordered sum) is formed while the late pair waits for its hand-off; after the
-  // late pair's y only the second halves remain.  The rule depends only on the block's graphs and
-  // the slot, so the fused, 3-launch and unfused launches agree bit for bit; sw = 0 (the plain
-  // row order) in every other block and whenever E = 0.
-  int E = -1;
-  if constexpr (GPB == 2 && SWARM_TD_SPLIT) {
-    const int i0 = __builtin_amdgcn_readfirstlane(TB.insl[0]), i1 = __builtin_amdgcn_readfirstlane(TB.insl[1]);
-    if ((i0 != 0) != (i1 != 0)) E = i0 != 0 ? 1 : 0;
-  }
-  const bool split = E >= 0;
-  const int sw = E == 1 ? 16 : 0;
-  const bool early = split && wi == E;
   const uint32_t tag = cc.tick + 1u;
   // granule address of this lane's node in a hand-off record: s at 0, s' at 4N, r at 8N, a at 9N
   auto ho_at = [&](int ct, int off, int per_node) -> const unsigned long long* {
@@ -577,28 +551,21 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   if (!online && !waited) __builtin_amdgcn_s_setprio(0);
   if (online && lane == 0) TB.prew[wi] = pre ? 1 : 0;
+  SWARM_STAMP(3);
+  __syncthreads();   // B1: TD targets
+  SWARM_STAMP(4);
 
   const float* P = Pon;
   float dz[CT][2][4];
-  // ---- the online wave's rows after y (after B1; a split block's early online wave as soon as
-  //      its target wave has y): dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ,
-  //      dZ = dR * [z > 0], the images of B2
-  auto online_dq = [&]() __attribute__((always_inline)) {
+  if (online) {
+    // ---- dQ at the taken action (MSELoss mean), dR = W2[a]^T dQ, dZ = dR * [z > 0]
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = 16 * ct + c, nn = min(n, NS - 1);
       if (FUSED && TB.tdrop[row0 + nn]) nv[ct] = false;   // the target wave dropped the graph
-      // Q at the taken action by register selects: the values pass an empty asm first, or the
-      // select chain becomes one load from a selected address and F goes to scratch memory
-      float qv[kActions];
+      float qa = F.q[ct][0];
 #pragma unroll
-      for (int a = 0; a < kActions; ++a) {
-        qv[a] = F.q[ct][a];
-        asm volatile("" : "+v"(qv[a]));
-      }
-      float qa = qv[0];
-#pragma unroll
-      for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? qv[a] : qa;
+      for (int a = 1; a < kActions; ++a) qa = (act[ct] == a) ? F.q[ct][a] : qa;
       const float delta = nv[ct] ? (qa - (rew[ct] + TB.yq[row0 + nn])) : 0.0f;   // y = r + gamma max Q_tgt(s')
       const float gq = delta * A.grad_scale;
 #pragma unroll
@@ -616,7 +583,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         TB.X[row][p] = F.x[ct][0];
         TB.X[row][4 + p] = F.x[ct][1];
 #pragma unroll
-        for (int j = 0; j < NS / 4; ++j) TB.cm_row(row)[4 * j + p] = pick4(F.cf[ct], j, p);
+        for (int j = 0; j < NS / 4; ++j) TB.cm[row][4 * j + p] = pick4(F.cf[ct], j, p);
         if (p == 0) { TB.X[row][8] = 0.0f; TB.gq[row] = gq; TB.d2[row] = delta * delta; }
       }
       if (pre) {   // the pre path's images scaled by this node's gq (rows free since B1)
@@ -634,14 +601,19 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const int u = 16 * ut + 4 * p + r;
-                if (u < NS) TB.dp_row(row0 + n)[u] = nv[ct] ? dp1[ct][ut][r] * gq : 0.0f;
+                if (u < NS) TB.dp[row0 + n][u] = nv[ct] ? dp1[ct][ut][r] * gq : 0.0f;
               }
           }
         }
         dad1[ct] = nv[ct] ? dad1[ct] * gq : 0.0f;
       }
     }
-  };
+  }
+  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph (pre path: dO / dp too)
+  SWARM_STAMP(5);
+  int np_pre = 0;   // online waves of this block on the pre path
+#pragma unroll
+  for (int w2 = 0; w2 < GPB; ++w2) np_pre += TB.prew[w2];
   // the parameter products that need only B2's images (each writes its slice of the slab).
   // dW1 = dZ^T T and dW2 = onehot(a) gq R as 16x16x4 MFMA tiles, K = 4 of the block's 32 node
   // rows per step: dW1 tiles (ti, tj) = jobs 2 ti + tj, dW2's 9 action rows in one 16-row tile
@@ -711,11 +683,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     }
   };
 
-
   const int col = lane & 31, h = lane >> 5;
-  // ---- the online wave's own rows after the images (after B2; a split block's early online
-  //      wave right after its images): the !pre dO / attention backward, then dh, da_src, da_dst
-  auto online_dh = [&]() __attribute__((always_inline)) {
+  if (online) {
     float da_d[CT];
     WSmall<NS>& sm = *V.sm;
 #pragma unroll
@@ -806,7 +775,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
               dpu = pre > 0.0f ? de : de * kLeakySlope;
             }
             dsum = dsum + dpu;
-            if (u < NS && v < NS) TB.dp_row(row0 + v)[u] = dpu;
+            if (u < NS && v < NS) TB.dp[row0 + v][u] = dpu;
           }
         da_d[ct] = row4_sum(dsum);
       }
@@ -834,7 +803,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         const int base = (GS < NS) ? (uu / GS) * GS : 0;
         float dpj[GS];   // read unconditionally (rows of this wave's graph), summed for j < N
 #pragma unroll
-        for (int j = 0; j < GS; ++j) dpj[j] = TB.dp_row(row0 + base + j)[uu];
+        for (int j = 0; j < GS; ++j) dpj[j] = TB.dp[row0 + base + j][uu];
 #pragma unroll
         for (int j = 0; j < GS; ++j) asm volatile("" : "+v"(dpj[j]));
 #pragma unroll
@@ -844,7 +813,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       f32x4 m0 = {0.f, 0.f, 0.f, 0.f}, m1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NS / 4; ++ks) {
-        const float b = TB.cm_row(row0 + 4 * ks + p)[uu];
+        const float b = TB.cm[row0 + 4 * ks + p][uu];
         m0 = mfma16(ao[0][ks], b, m0);
         m1 = mfma16(ao[1][ks], b, m1);
       }
@@ -861,196 +830,25 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
     SWARM_STAMP(27);
-  };
-  // split blocks: the same row sums in two halves of the K order (rows (16 hh + k) ^ sw); the
-  // accumulators carry over between the halves, so the result is that of one pass in that order
-  auto b2_tiles_h = [&](int tj, int hh, f32x4 (&dd)[3]) __attribute__((always_inline)) {
-    float a1[2][4], b1[4], a2[4], b2v[4];
-    int an[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int n = (16 * hh + 4 * s + p) ^ sw;
-      a1[0][s] = TB.dZ[n][c];
-      a1[1][s] = TB.dZ[n][16 + c];
-      b1[s] = TB.T[n][16 * tj + c];
-      b2v[s] = TB.R[n][16 * tj + c];
-      an[s] = TB.act[n];
-      a2[s] = TB.gq[n];
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      dd[0] = mfma16(a1[0][s], b1[s], dd[0]);
-      dd[1] = mfma16(a1[1][s], b1[s], dd[1]);
-      dd[2] = mfma16(an[s] == c ? a2[s] : 0.0f, b2v[s], dd[2]);
-    }
-  };
-  auto b2_tiles_st = [&](int tj, const f32x4 (&dd)[3]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sst(OFF_W1 + (4 * p + r) * kHidden + 16 * tj + c, dd[0][r]);
-      sst(OFF_W1 + (16 + 4 * p + r) * kHidden + 16 * tj + c, dd[1][r]);
-      if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, dd[2][r]);
-    }
-  };
-  // the ordered vector sums, half hh: B2's db1 (b3 = false, job 2) and db2 + loss (job 3), B3's
-  // att_src / att_dst (b3, job 2) and dbias (job 3)
-  auto vsum_h = [&](int job, bool b3, int hh, float& acc) __attribute__((always_inline)) {
-    if (!b3 && job == 2) {
-      if (lane < kHidden) {
-        float v[16];
-#pragma unroll
-        for (int n = 0; n < 16; ++n) v[n] = TB.dZ[(16 * hh + n) ^ sw][lane];
-#pragma unroll
-        for (int n = 0; n < 16; ++n) acc = (hh == 0 && n == 0) ? v[n] : acc + v[n];
-      }
-    } else if (!b3) {
-      if (lane < kActions || lane == 63) {
-#pragma unroll
-        for (int k = 0; k < 16; k += 8) {
-          int a8[8];
-          float g8[8], d8[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int n = (16 * hh + k + j) ^ sw;
-            a8[j] = TB.act[n]; g8[j] = TB.gq[n]; d8[j] = TB.d2[n];
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(g8[j]), "+v"(d8[j]));
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float v = lane == 63 ? d8[j] : (a8[j] == lane ? g8[j] : 0.0f);
-            acc = (hh == 0 && k == 0 && j == 0) ? v : acc + v;
-          }
-        }
-      }
-    } else if (job == 2) {
-      const float* da = h == 0 ? TB.das : TB.dad;
-      float v[16];
-#pragma unroll
-      for (int n = 0; n < 16; ++n) {
-        const int m = (16 * hh + n) ^ sw;
-        v[n] = da[m] * TB.H[m][col];
-      }
-#pragma unroll
-      for (int n = 0; n < 16; ++n) acc = (hh == 0 && n == 0) ? v[n] : acc + v[n];
-    } else if (lane < kHidden) {
-      float v[16];
-#pragma unroll
-      for (int n = 0; n < 16; ++n) v[n] = TB.dO[(16 * hh + n) ^ sw][lane];
-#pragma unroll
-      for (int n = 0; n < 16; ++n) acc = (hh == 0 && n == 0) ? v[n] : acc + v[n];
-    }
-  };
-  auto vsum_st = [&](int job, bool b3, float acc) __attribute__((always_inline)) {
-    if (!b3 && job == 2) {
-      if (lane < kHidden) sst(OFF_B1 + lane, acc);
-    } else if (!b3) {
-      if (lane < kActions || lane == 63) sst(lane == 63 ? N_PARAMS : OFF_B2 + lane, acc);
-    } else if (job == 2) {
-      sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, acc);
-    } else if (lane < kHidden) {
-      sst(OFF_BIAS + lane, acc);
-    }
-  };
-  auto dw_h = [&](int t, int hh, f32x4& acc) __attribute__((always_inline)) {   // dW rows 16 t .. 16 t + 15 (B3 job t), half hh
-    float ha[4], xb[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int n = (16 * hh + 4 * ks + p) ^ sw;
-      ha[ks] = TB.dH[n][16 * t + c];
-      xb[ks] = TB.X[n][c < kFeat ? c : 8];
-    }
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) acc = mfma16(ha[ks], xb[ks], acc);
-  };
-  auto dw_st = [&](int t, const f32x4& acc) __attribute__((always_inline)) {
-    if (c < kFeat) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sst(OFF_W + (16 * t + 4 * p + r) * kFeat + c, acc[r]);
-    }
-  };
-
-  // ---- split block, early pair: its target wave's y -> its online wave's images and dH -> the
-  //      first half of every product, before B1: the target wave takes column half 0 of the B2
-  //      tiles, db1, dW rows 0-15 and att; the online wave column half 1, db2 + loss, dW rows 16-31
-  //      and dbias.  The same waves finish them after B2 / B3, on a path of their own with its
-  //      own three barriers (every wave of the block passes three), so that the partial sums they
-  //      carry are not live across the late waves' backward
-  if (early) {
-    const int xj = online ? 1 : 0;
-    if (!online) {
-      lds_flag_set(&TB.fl[0]);   // y of the early rows
-      lds_flag_wait(&TB.fl[1]);
-    } else {
-      lds_flag_wait(&TB.fl[0]);
-      online_dq();
-      lds_flag_set(&TB.fl[1]);   // dZ / gq / act / d2 / X / cm / dO / dp of the early rows
-      wave_lds_sync();
-      online_dh();
-      wave_lds_sync();
-      lds_flag_set(&TB.fl[2]);   // dH / das / dad of the early rows
-    }
-    f32x4 xd[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    f32x4 xw = {0.f, 0.f, 0.f, 0.f};
-    float xs = 0.0f, xt = 0.0f;
-    b2_tiles_h(xj, 0, xd);
-    vsum_h(2 + xj, false, 0, xs);
-    if (!online) lds_flag_wait(&TB.fl[2]);
-    dw_h(xj, 0, xw);
-    vsum_h(2 + xj, true, 0, xt);
-    SWARM_STAMP(3);
-    __syncthreads();   // B1 (early path)
-    SWARM_STAMP(4);
-    __syncthreads();   // B2 (early path): the late rows' images
-    SWARM_STAMP(5);
-    b2_tiles_h(xj, 1, xd);
-    b2_tiles_st(xj, xd);
-    vsum_h(2 + xj, false, 1, xs);
-    vsum_st(2 + xj, false, xs);
-    SWARM_STAMP(26);
-    __syncthreads();   // B3 (early path): the late rows' dH
-    SWARM_STAMP(6);
-    dw_h(xj, 1, xw);
-    dw_st(xj, xw);
-    vsum_h(2 + xj, true, 1, xt);
-    vsum_st(2 + xj, true, xt);
   } else {
-  SWARM_STAMP(3);
-  __syncthreads();   // B1: TD targets
-  SWARM_STAMP(4);
-  if (online) online_dq();
-  __syncthreads();   // B2: dZ / T / R / gq / act / d2 / X / cm of every graph (pre path: dO / dp too)
-  SWARM_STAMP(5);
-  if (split) {   // the late online wave's dH beside the early waves' second halves
-    if (online) online_dh();
-  } else {
-    int np_pre = 0;   // online waves of this block on the pre path
-#pragma unroll
-    for (int w2 = 0; w2 < GPB; ++w2) np_pre += TB.prew[w2];
-    if (online) {
-      online_dh();
-    } else {
-      // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
-      //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
-      //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
-      for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
-      if (np_pre == 0)
-        for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
-    }
-    if (online && pre) {   // (GPB = 2: one pre wave takes both sums, two split them)
-      if (np_pre == 1 || wi == 0) b2_job(2);
-      if (np_pre == 1 || wi == 1) b2_job(3);
-    }
+    // ---- target waves: the dW1 / dW2 tiles of column half tj = wi (GPB = 2) or both (GPB = 1);
+    //      the vector sums (db1, db2 + loss) too unless the block has pre-path online waves:
+    //      theirs is the short side of B2 -> B3 there, and the target waves' products the long one
+    for (int tj = wi; tj < 2; tj += GPB) b2_tiles(tj);
+    if (np_pre == 0)
+      for (int job = 2 + wi; job < 4; job += GPB) b2_job(job);
+  }
+  if (online && pre) {   // (GPB = 2: one pre wave takes both sums, two split them)
+    if (np_pre == 1 || wi == 0) b2_job(2);
+    if (np_pre == 1 || wi == 1) b2_job(3);
   }
   SWARM_STAMP(26);   // stamps build: the B2 jobs done, before the B3 wait
   __syncthreads();   // B3: dO / dH / das / dad
   SWARM_STAMP(6);
-  if (!split) {
-    // ---- products over B3's images, spread over all 2 GPB waves of the block:
-    //      job 0 / 1: dW rows 0-15 / 16-31 = sum_n dH[n][f] X[n][k] (MFMA 16x16x4, K = node rows)
-    //      job 2: att_src / att_dst (lane halves) ; job 3: dbias
+  // ---- products over B3's images, spread over all 2 GPB waves of the block:
+  //      job 0 / 1: dW rows 0-15 / 16-31 = sum_n dH[n][f] X[n][k] (MFMA 16x16x4, K = node rows)
+  //      job 2: att_src / att_dst (lane halves) ; job 3: dbias
+  {
     const int wall = online ? wi : GPB + wi;
     for (int job = wall; job < 4; job += 2 * GPB) {
       if (job < 2) {
@@ -1091,7 +889,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
   }
-  }   // !early
   SWARM_STAMP(7);
   SWARM_RTSTAMP(9);
 }
