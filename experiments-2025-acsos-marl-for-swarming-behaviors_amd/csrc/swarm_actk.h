@@ -272,42 +272,6 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
   // same hoist measured slower at C3 (18.17 -> 18.82 us per tick, 66 instead of 45 SGPR spills:
   // profiles/r05_ab_hoist_forces_c3.jsonl), so there the forces keep their place after the argmax
   if (MODE != MODE_Q && kHoist) pair_forces();
-  // Fused tick (hoisted forces): the force sum and the integrator for each of the three levels
-  // an axis's action can take (the x and y updates never mix, action_level(a / 3) and
-  // action_level(a % 3)), formed here in the same wait.  Each candidate is the same operation
-  // sequence as after the argmax (0 + level, the obstacle pair, the partners in VMAS order, drag
-  // + Euler), so the chosen one is that value bit for bit; between the argmax and the s'
-  // hand-off only a select remains
-  constexpr bool kCand = kHoist && MODE == MODE_TICK;
-  float cp[CT][2][3], cv[CT][2][3];   // [node column][axis][level]: p', v'
-  if constexpr (kCand) {
-    wave_lds_sync();
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int n = min(16 * ct + c, NS - 1);
-      float2 ob = make_float2(0.0f, 0.0f);
-      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) ob = *reinterpret_cast<const float2*>(fb + kFbOb + 2 * n);
-      float2 f[NS];
-#pragma unroll
-      for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + n * kFbRow + 2 * u);
-#pragma unroll
-      for (int l = 0; l < 3; ++l) {
-        float fx = 0.0f + action_level(l);
-        float fy = 0.0f + action_level(l);
-        if (SCEN == SWARM_OBSTACLE_AVOIDANCE) { fx = fx + ob.x; fy = fy + ob.y; }
-#pragma unroll
-        for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
-        integrate_axis(px[ct], vx[ct], fx, cp[ct][0][l], cv[ct][0][l]);
-        integrate_axis(py[ct], vy[ct], fy, cp[ct][1][l], cv[ct][1][l]);
-      }
-      // formed HERE: without the empty asm the compiler sinks the sums to their use after the
-      // argmax, back onto the chain
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int l = 0; l < 3; ++l) asm volatile("" : "+v"(cp[ct][k][l]), "+v"(cv[ct][k][l]));
-    }
-  }
   // ...and the first tick's random actions of an exploring env (train_gcn_dqn.py:164-165)
   int ract0[CT];
 #pragma unroll
@@ -422,46 +386,31 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
     //      index; -f(p_u - p_v) == f(p_v - p_u) bit for bit.
     if (MODE != MODE_Q && !kHoist) pair_forces();   // (16 slots: here, after the argmax)
     if (it == 0) SWARM_STAMP(6);
-    if (!kCand) wave_lds_sync();
+    wave_lds_sync();
     if (it == 0) SWARM_STAMP(7);
     StepOut o[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int n = min(16 * ct + c, NS - 1);
-      if constexpr (kCand) {   // the candidates of the prologue: the action's levels select
-        // (register selects on copies that pass an empty asm: a select chain over the array
-        // would become one load from a selected address and move the candidates to memory)
-        auto sel3 = [](int k, float a0, float a1, float a2) {
-          asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2));
-          return k == 0 ? a0 : (k == 1 ? a1 : a2);
-        };
-        const int ax = action[ct] / 3, ay = action[ct] % 3;
-        o[ct].px = sel3(ax, cp[ct][0][0], cp[ct][0][1], cp[ct][0][2]);
-        o[ct].vx = sel3(ax, cv[ct][0][0], cv[ct][0][1], cv[ct][0][2]);
-        o[ct].py = sel3(ay, cp[ct][1][0], cp[ct][1][1], cp[ct][1][2]);
-        o[ct].vy = sel3(ay, cv[ct][1][0], cv[ct][1][1], cv[ct][1][2]);
-      } else {
-        float fx = 0.0f + action_level(action[ct] / 3);
-        float fy = 0.0f + action_level(action[ct] % 3);
-        if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {   // the obstacle pair (pair_forces)
-          const float2 g = *reinterpret_cast<const float2*>(fb + kFbOb + 2 * n);
-          fx = fx + g.x; fy = fy + g.y;
-        }
-        // every slot read at once, no per-partner branch: slots u >= N hold +0 and fx, fy
-        // (started from +0 or +-1) never become -0, so adding them is exact
-        float2 f[NS];
-#pragma unroll
-        for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + n * kFbRow + 2 * u);
-#pragma unroll
-        for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
-        o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
+      float fx = 0.0f + action_level(action[ct] / 3);
+      float fy = 0.0f + action_level(action[ct] % 3);
+      if (SCEN == SWARM_OBSTACLE_AVOIDANCE) {   // the obstacle pair (pair_forces)
+        const float2 g = *reinterpret_cast<const float2*>(fb + kFbOb + 2 * n);
+        fx = fx + g.x; fy = fy + g.y;
       }
+      // every slot read at once, no per-partner branch: slots u >= N hold +0 and fx, fy
+      // (started from +0 or +-1) never become -0, so adding them is exact
+      float2 f[NS];
+#pragma unroll
+      for (int u = 0; u < NS; ++u) f[u] = *reinterpret_cast<const float2*>(fb + n * kFbRow + 2 * u);
+#pragma unroll
+      for (int u = 0; u < NS; ++u) { fx = fx + f[u].x; fy = fy + f[u].y; }
+      o[ct] = integrate(px[ct], py[ct], vx[ct], vy[ct], fx, fy);
       if (MODE == MODE_TICK && HO && ho_r && valid[ct]) {
         const int nn = 16 * ct + c;
         const float v = p == 0 ? o[ct].px : (p == 1 ? o[ct].py : (p == 2 ? o[ct].vx : o[ct].vy));
         st_granule(ho_r + 4 * N + 4 * nn + p, ho_tag, __float_as_uint(v));
       }
-      if constexpr (kCand) step_distances(o[ct]);   // after s' is on its way
       if (16 * ct + c < NS && p == 0) {
         if (SCEN == SWARM_FLOCKING) { sm.aux[16 * ct + c] = o[ct].px; sm.aux2[16 * ct + c] = o[ct].py; }
         else { sm.aux[16 * ct + c] = o[ct].dgoal; sm.aux2[16 * ct + c] = (o[ct].dobs <= 0.2f) ? 1.0f : 0.0f; }

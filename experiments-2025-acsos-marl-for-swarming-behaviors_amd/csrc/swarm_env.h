@@ -15,23 +15,16 @@ struct StepOut {
 
 // Drag + Euler and the scenario distances of one agent after its force sum (VMAS
 // World._integrate_state, dt 0.1, drag 0.25, mass 1).
-// One axis of the integrator (the x and y updates never mix): v' = v drag + (f / m) dt,
-// p' = p + v' dt.
-__device__ inline void integrate_axis(float p, float v, float f, float& p1, float& v1) {
-  v1 = v * kDragKeep;
-  v1 = v1 + (f / 1.0f) * kDt;
-  p1 = p + v1 * kDt;
-}
-// the scenario distances of the new position
-__device__ inline void step_distances(StepOut& o) {
-  o.dgoal = norm2(o.px - kGoalX, o.py - kGoalY);
-  o.dobs = (norm2(o.px - kObstX, o.py - kObstY) - kRadius) - kRadius;
-}
 __device__ inline StepOut integrate(float px, float py, float vx, float vy, float fx, float fy) {
   StepOut o;
-  integrate_axis(px, vx, fx, o.px, o.vx);
-  integrate_axis(py, vy, fy, o.py, o.vy);
-  step_distances(o);
+  o.vx = vx * kDragKeep;
+  o.vy = vy * kDragKeep;
+  o.vx = o.vx + (fx / 1.0f) * kDt;
+  o.vy = o.vy + (fy / 1.0f) * kDt;
+  o.px = px + o.vx * kDt;
+  o.py = py + o.vy * kDt;
+  o.dgoal = norm2(o.px - kGoalX, o.py - kGoalY);
+  o.dobs = (norm2(o.px - kObstX, o.py - kObstY) - kRadius) - kRadius;
   return o;
 }
 
