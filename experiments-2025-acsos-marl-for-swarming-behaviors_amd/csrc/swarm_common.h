@@ -187,9 +187,10 @@ __host__ __device__ inline size_t slab_index(int q, int b, int n_slabs) {
 // Record of env e (granule index): s [N][4] at 4n + k, s' [N][4] at 4N + 4n + k, r at 8N + n,
 // a at 9N + n.
 __host__ __device__ constexpr int ho_stride_granules(int N) { return ((10 * N + 15) / 16) * 16; }
-// Through global-address-space pointers: global_load / global_store count in vmcnt only,
-// where flat ones also hold lgkmcnt, so an LDS wait after a granule store (the acting wave's
-// s, a and s' publishes are followed by LDS syncs) would also wait for its write-through
+// Through global-address-space pointers: the TD waves' polls read the record through a pointer
+// the compiler cannot trace to a kernel argument, so they were flat loads, which count in lgkmcnt
+// as well as vmcnt (a wait for a poll then also drained the wave's LDS operations, and an LDS
+// wait the poll).  As global loads they count in vmcnt only
 typedef __attribute__((address_space(1))) unsigned long long gran_t;
 __device__ inline void st_granule(unsigned long long* g, uint32_t tag, uint32_t value) {
   __hip_atomic_store((gran_t*)g, ((unsigned long long)tag << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
