@@ -108,11 +108,6 @@ struct TdFused {
 #ifndef SWARM_HO_SLEEP
 #define SWARM_HO_SLEEP 1  // s_sleep argument (x 64 cycles) between two hand-off sweeps
 #endif
-#ifndef SWARM_HO_DEPTH
-#define SWARM_HO_DEPTH 2   // hand-off sweeps in flight in a wave's s / s' wait: 1 or 2
-#endif
-constexpr int kHoDepth = SWARM_HO_DEPTH;
-static_assert(kHoDepth == 1 || kHoDepth == 2, "SWARM_HO_DEPTH");
 constexpr int kHoSpinLimit = SWARM_HO_SPIN_LIMIT;   // polls (with s_sleep) before a hand-off wait gives up
 // test builds only (libswarm_hip_hodrop.so): every hand-off wait overruns at once
 constexpr bool kHoForceDrop = SWARM_HO_FORCE_DROP == 1;
@@ -332,50 +327,29 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   if (waited) {   // sweep this lane's granules until every tag is this tick's (R2 hand-off): online
                   // waves s (published at the acting prologue), target waves s' (after the integrator).
                   // Wave-local, after B0: the block's other waves are not held by it
-    // Two sweeps in flight (SWARM_HO_DEPTH 2): the next sweep is issued before the older one is
-    // checked, so a granule that lands while a sweep is out is seen about one round trip later,
-    // not up to two.  Two buffers used in turn (a copy of a sweep still in flight would wait for
-    // it); every lane loads and the tag test has no branch, so each check waits for its own sweep
-    // only
-    unsigned long long qa[CT][4], qb[CT][4];
-    // A lane whose graph is not a hand-off graph loads the granules of the lane 8 columns over
-    // (the same node of the wave's other graph when GS = 8): the same addresses as a lane that
-    // needs them, so the wave's loads coalesce and the sweep adds no traffic
-    const unsigned long long* spl[CT];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      uint32_t lg = gid[ct];
-      if constexpr (GS < 16) {
-        const uint32_t og = (uint32_t)__shfl_xor((int)gid[ct], GS);
-        lg = ho[ct] ? gid[ct] : og;
-      }
-      spl[ct] = ho_rec + (size_t)(lg % (uint32_t)B) * ho_stride_granules(N) + (online ? 0 : 4 * N) +
-                4 * min(jl[ct], N - 1);
-    }
-    auto sweep = [&](unsigned long long (&g)[CT][4]) {
+    for (int spin = 0;; ++spin) {
+      unsigned long long g[CT][4];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
+        if (ho[ct]) {
+          const unsigned long long* sp = ho_at(ct, online ? 0 : 4 * N, 4);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[ct][k] = ld_granule(spl[ct] + k);
-    };
-    // true when the wait is over: every granule carries this tick's tag, or the bound ran out
-    auto check = [&](const unsigned long long (&g)[CT][4], int spin) -> bool {
+          for (int k = 0; k < 4; ++k) g[ct][k] = ld_granule(sp + k);
+        }
       bool ok = true, okc[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        const bool tags = ((uint32_t)(g[ct][0] >> 32) == tag) & ((uint32_t)(g[ct][1] >> 32) == tag) &
-                          ((uint32_t)(g[ct][2] >> 32) == tag) & ((uint32_t)(g[ct][3] >> 32) == tag);
-        okc[ct] = !ho[ct] || (!kHoForceDrop && !(kHoDropTarget && !online) && tags);
-        ok = ok & okc[ct];
+        okc[ct] = true;
+        if (ho[ct]) {
+          okc[ct] = !kHoForceDrop && !(kHoDropTarget && !online) && (uint32_t)(g[ct][0] >> 32) == tag &&
+                    (uint32_t)(g[ct][1] >> 32) == tag && (uint32_t)(g[ct][2] >> 32) == tag &&
+                    (uint32_t)(g[ct][3] >> 32) == tag;
+          ok = ok && okc[ct];
+          st[ct] = make_float4(__uint_as_float((uint32_t)g[ct][0]), __uint_as_float((uint32_t)g[ct][1]),
+                               __uint_as_float((uint32_t)g[ct][2]), __uint_as_float((uint32_t)g[ct][3]));
+        }
       }
-      if (ok) {   // (wave-uniform) this sweep is the data
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          if (ho[ct])
-            st[ct] = make_float4(__uint_as_float((uint32_t)g[ct][0]), __uint_as_float((uint32_t)g[ct][1]),
-                                 __uint_as_float((uint32_t)g[ct][2]), __uint_as_float((uint32_t)g[ct][3]));
-      }
-      if (!__builtin_amdgcn_ballot_w64(!ok)) return true;
+      if (!__builtin_amdgcn_ballot_w64(!ok)) break;
       if (kHoForceDrop || (kHoDropTarget && !online) || spin >= kHoSpinLimit) {   // never in a correct
         if (lane == 0) atomicAdd(X.ho_err, 1u);                                   // run: count, drop
         drop_overrun<NS, GS>(okc, live_drop, nv, c);
@@ -384,36 +358,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
           for (int ct = 0; ct < CT; ++ct)
             if (16 * ct + c < NS && live_drop[ct]) *(volatile int*)&TB.tdrop[row0 + 16 * ct + c] = 1;
         }
-        return true;
+        break;
       }
-      return false;
-    };
-    if constexpr (kHoDepth == 1) {
-      for (int spin = 0;; ++spin) {
-        sweep(qa);
-        if (check(qa, spin)) break;
-        __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
-      }
-    } else {
-      // the first 16 checks in straight-line code (a loop back-edge makes the wait before the
-      // first check of an iteration vmcnt(0), which waits for the younger sweep too), then a loop
-      sweep(qa);
-      do {
-#pragma unroll
-        for (int k = 0; k < 16; k += 2) {
-          sweep(qb);
-          if (check(qa, k)) goto ho_done;
-          sweep(qa);
-          if (check(qb, k + 1)) goto ho_done;
-        }
-        for (int spin = 16;; spin += 2) {
-          sweep(qb);
-          if (check(qa, spin)) break;
-          sweep(qa);
-          if (check(qb, spin + 1)) break;
-        }
-      } while (0);
-    ho_done:;
+      __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
     }
     SWARM_RTSTAMP(10);
     __builtin_amdgcn_s_setprio(3);   // waves of hand-off graphs are the tick's critical path
