@@ -167,10 +167,16 @@ def spawn_ranks(argv, n: int, script: str = None) -> int:
     """Start n ranks as a child process (never an exec: this process has not touched the GPU and
     stays the parent), relay their stdout line by line, and return non-zero if the launcher fails
     or rank 0's JSON line does not report n GPUs."""
+    import signal
     cmd = rank_launch_cmd(argv, n, free_port(), script)
     print("[bench] starting %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
-    # own session: on any exit of the relay other than its normal end (an exception, ^C, SIGTERM
-    # turned into SystemExit) the whole launcher process group is terminated, ranks included
+    # own session: on any exit of the relay other than its normal end (an exception, ^C, SIGTERM or
+    # SIGHUP, which the handlers below turn into SystemExit) the whole launcher process group is
+    # terminated, ranks included; the ranks are outside the caller's process group, so without
+    # the handlers a SIGTERM to the relay would orphan them (ADVICE r5)
+    def _exit_on(signum, _frame):
+        raise SystemExit(128 + signum)
+    old = {sig: signal.signal(sig, _exit_on) for sig in (signal.SIGTERM, signal.SIGHUP)}
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)
     line = None
     done = False
@@ -190,6 +196,8 @@ def spawn_ranks(argv, n: int, script: str = None) -> int:
     finally:
         if not done:
             stop_group(proc)
+        for sig, h in old.items():
+            signal.signal(sig, h)
     if rc != 0:
         print(f"[bench] rank launcher exited with {rc}", file=sys.stderr)
         return rc
@@ -237,7 +245,18 @@ def main():
         torch.distributed.barrier()
 
     build = lib_identity()
-    peer, allreduce = None, None
+    B, N = args.envs, args.agents
+    shard = swdist.Shard(rank, world, B)
+    S = args.batch or B
+    scen = args.scenario
+    if args.net == "gat3":
+        if args.mode != "act":
+            raise SystemExit("--net gat3 is forward only: use --mode act")
+        w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "flocking_weights.npz"))["weights_flocking"][0])
+    else:   # Flocking trains the one-layer network: start it from GoTo's checkpoint
+        wkey = "weights_obstacle_avoidance" if scen == "ObstacleAvoidance" else "weights_go_to"
+        w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
+    peer, allreduce, fused_check = None, None, None
     if distributed and args.mode == "train":
         allreduce = "rccl" if args.backend == "nccl" else args.backend
         if args.allreduce != "rccl":
@@ -253,25 +272,31 @@ def main():
                                 device="cuda" if args.backend == "nccl" else "cpu")
             torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
             if int(flag.item()) == 1:
+                # VERDICT r5 "next" #2: before any timed tick, the exchange the line will time runs on
+                # THIS library: fused training ticks of the run's own configuration through
+                # swarm_reduce_advance_peer (the shipped reduce geometry), every rank's gradient checked
+                # bitwise against the rank-ordered sum of the ranks' own column sums, error words 0
+                try:
+                    fused_check = peer.fused_selftest(lambda p: swarm_amd.SwarmEngine(
+                        scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=shard.env_offset,
+                        world_size=world, process_group=pg, update_target_every=2, replay_capacity=3 * B,
+                        conv=args.conv, graph=args.graph, knn_k=args.knn_k, radius=args.radius, peer=p), pg)
+                except RuntimeError as e:
+                    fused_check = {"ok": False, "why": str(e)}
+                flag.fill_(1 if fused_check["ok"] else 0)
+                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+                fused_check["all_ranks_ok"] = int(flag.item()) == 1
+                if not fused_check["ok"]:
+                    why = f"fused exchange check: {fused_check}"
+            if int(flag.item()) == 1:
                 allreduce = "xGMI peer stores fused into the slab reduce (swarm_reduce_advance_peer)"
             else:
                 if args.allreduce == "peer":
                     raise SystemExit(f"rank {rank}: peer all-reduce self-test failed ({why or 'wrong sums'})")
-                print(f"[bench] rank {rank}: peer all-reduce self-test failed ({why or 'wrong sums'}); "
+                print(f"[bench] rank {rank}: peer all-reduce self-test failed ({why or 'wrong sums on a peer rank'}); "
                       f"falling back to {allreduce}", file=sys.stderr)
                 peer = None
 
-    B, N = args.envs, args.agents
-    shard = swdist.Shard(rank, world, B)
-    S = args.batch or B
-    scen = args.scenario
-    if args.net == "gat3":
-        if args.mode != "act":
-            raise SystemExit("--net gat3 is forward only: use --mode act")
-        w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "flocking_weights.npz"))["weights_flocking"][0])
-    else:   # Flocking trains the one-layer network: start it from GoTo's checkpoint
-        wkey = "weights_obstacle_avoidance" if scen == "ObstacleAvoidance" else "weights_go_to"
-        w0 = torch.tensor(np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))[wkey][0])
     eng = swarm_amd.SwarmEngine(scen, N, B, seed=0, params=w0, batch=S, eps=0.05, env_offset=shard.env_offset,
                                 world_size=world, process_group=pg, update_target_every=200,
                                 replay_capacity=1_000_000 if args.net == "gcn" else 1, conv=args.conv,
@@ -494,6 +519,10 @@ def main():
         acting = acting_leg(argparse.Namespace(**{**vars(args), "graph": "knn", "knn_k": k_eval}), e_knn, max_steps)
         del e_knn
         acting["training_graph"] = acting_leg(args, eng, max_steps)
+        # the basis of this key changed in round 5; say so in the line itself
+        acting["headline_graph"] = (f"kNN-{k_eval}: the reference's evaluation graph (simulator.py:15-24), the "
+                                    "basis of acting_only.value since round 5; rounds 1-4 quoted the training "
+                                    "graph's rollout, which is acting_only.training_graph")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -514,7 +543,8 @@ def main():
                                           " + xGMI peer grad all-reduce" if peer is not None else
                                           f" + {'RCCL' if args.backend == 'nccl' else args.backend} grad all-reduce"),
                            "hipgraph": graph is not None, "tick": "1 launch + reduce" if fused else "3 launches",
-                           "allreduce": allreduce, "allreduce_paths": both, "rank_errors": rank_errors,
+                           "allreduce": allreduce, "allreduce_paths": both, "peer_fused_check": fused_check,
+                           "rank_errors": rank_errors,
                            "replicas_identical": replicas},
                 "roofline": roof, "cpu_baseline": cpu, "acting_only": acting, "build": build,
                 "loss": ctrl["loss"]}

@@ -351,13 +351,16 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
       if (kHoForceDrop || (kHoDropTarget && !online) || spin >= kHoSpinLimit) {   // never in a correct
-        if (lane == 0) atomicAdd(X.ho_err, 1u);                                   // run: count, drop
-        drop_overrun<NS, GS>(okc, live_drop, nv, c);
-        if (FUSED && !online && p == 0) {   // tell the online waves' r wait (they do not count it again)
+        drop_overrun<NS, GS>(okc, live_drop, nv, c);                              // run: drop, count
+        // tell the online waves' r wait first (they then drop without counting again), count after.
+        // An online wave whose own r wait overruns BEFORE this store counts the graph as well: the
+        // error word counts dropping waves, and is nonzero whenever a graph was dropped
+        if (FUSED && !online && p == 0) {
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct)
             if (16 * ct + c < NS && live_drop[ct]) *(volatile int*)&TB.tdrop[row0 + 16 * ct + c] = 1;
         }
+        if (lane == 0) atomicAdd(X.ho_err, 1u);
         break;
       }
       __builtin_amdgcn_s_sleep(SWARM_HO_SLEEP);
@@ -516,8 +519,8 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
       if (!__builtin_amdgcn_ballot_w64(!ok)) break;
       if (kHoForceDrop || spin >= kHoSpinLimit) {   // the graph's rows are dropped (online side)
-        // graphs the target wave has dropped already (its s' wait overran; LDS flag set before its
-        // count) are dropped here too but not counted a second time
+        // graphs the target wave has dropped already (its s' wait overran; the LDS flag is stored
+        // before its count) are dropped here too but not counted a second time
         bool rest = false;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {

@@ -228,6 +228,56 @@ class PeerExchange:
             ok = bool(torch.equal(x, want)) and self.errors() == 0
         return ok
 
+    def fused_selftest(self, make_engine, group=None, ticks: int = 4) -> dict:
+        """The exchange the timed ticks will run, executed before them on THIS library (VERDICT r5
+        "next" #2): ``make_engine(peer)`` builds a throwaway engine of the run's configuration
+        (same envs, agents and TD batch, hence the same tick kernel, slab count and reduce
+        geometry) on this exchange; ``ticks`` training ticks then go through
+        ``swarm_reduce_advance_peer`` (grad_reduce_kernel<1>: slab sum, peer stores, rank-ordered
+        sum).  After each, this rank's own column sums of the same slabs (``swarm_grad_reduce``:
+        the same geometry, no exchange) are gathered over ``group`` and the gradient every rank
+        holds must equal their rank-ordered fp32 sum bit for bit; the expired-wait word, the
+        hand-off word and ctrl.peer_hold must stay 0.  Collective: every rank calls it.  Returns
+        {"ok": bool, ...details}; the caller MIN-reduces "ok" over the ranks and falls back."""
+        import ctypes
+        import torch.distributed as dist
+        from . import _lib
+        from ._lib import CTRL, N_PARAMS, check, ptr, stream_ptr
+        if self.error is not None:
+            return {"ok": False, "why": str(self.error)}
+        eng = make_engine(self)
+        if eng.peer is not self:
+            raise ValueError("fused_selftest: make_engine must build its engine on this exchange")
+        dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        local = torch.zeros_like(eng.grad)
+        res, nonzero = [], 0
+        st = self._stream if self._stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(st):   # this rank's one peer stream (check_stream)
+            eng.reset(0)
+            for t in range(ticks):
+                eng.train_tick()
+                check(self.lib.swarm_grad_reduce(ctypes.byref(eng.cfg), ctypes.byref(eng.hp), ptr(eng.slabs),
+                                                 ptr(local), stream_ptr()), "swarm_grad_reduce")
+                torch.cuda.synchronize(self.device)
+                mine = local[:N_PARAMS + 1].clone()
+                allv = [torch.zeros_like(mine, device=dev) for _ in range(self.world_size)]
+                dist.all_gather(allv, mine.to(dev), group=group)
+                want = allv[0].clone()
+                for q in range(1, self.world_size):
+                    want = want + allv[q]   # rank order, fp32
+                got = eng.grad[:N_PARAMS + 1].to(dev)
+                res.append(bool(torch.equal(got, want)))
+                nonzero += int(bool(mine.abs().sum() > 0))
+            eng.flush()
+            torch.cuda.synchronize(self.device)
+        out = {"ok": all(res) and nonzero > 0 and self.errors() == 0 and eng.handoff_errors() == 0
+               and int(eng.ctrl[CTRL["peer_hold"]].item()) == 0,
+               "ticks": ticks, "bitwise": sum(res), "trained_ticks": nonzero, "expired_waits": self.errors(),
+               "handoff_overruns": eng.handoff_errors(), "peer_hold": int(eng.ctrl[CTRL["peer_hold"]].item()),
+               "reduce_geometry": _lib.load().swarm_build_info().decode()}
+        del eng
+        return out
+
     def close(self):
         from ._lib import check
         import ctypes

@@ -179,7 +179,10 @@ class SwarmEngine:
             check(int(ws), "swarm_td_workspace_floats")
         self.fused = learn and bool(self.lib.swarm_train_tick_supported(ctypes_ref(self.cfg)))
         self.slabs = torch.zeros(int(ws), **f32)
-        self.grad = torch.zeros(_lib.GRAD_FLOATS, **f32)   # + the reduce's norm partials (ABI 10)
+        # + the reduce's norm partials (ABI 10); a write to grad from outside the library's reduce
+        # must be declared with grad_written() (the partials then no longer describe it)
+        self.grad = torch.zeros(_lib.GRAD_FLOATS, **f32)
+        self._grad_dirty = False
         self.learner = SwarmLearner(*[ptr(self._lrn[i]) for i in range(7)], ptr(self.grad))
         self.samples = torch.zeros(max(self.batch, 1), dtype=torch.int32, device=dev)
         # fused-tick workspace (error word, launch counters, hand-off granule records); zeroed with ctrl
@@ -265,14 +268,25 @@ class SwarmEngine:
         check(self.lib.swarm_td_grad(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.params), ptr(self.target),
                                      ctypes_ref(self.replay), ptr(self.ctrl), ptr(sample_in), ptr(sample_out),
                                      ptr(self.slabs), stream_ptr()), "swarm_td_grad")
+        self._grad_dirty = False
         check(self.lib.swarm_grad_reduce(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
     def _sync_flags(self):
         """swarm_adam_cfg.flags for the next launches: the reduce's clip-norm partials describe
-        lr->grad unless an all-reduce of the gradient (RCCL / gloo / by hand) follows the reduce."""
-        exact = self.world_size == 1 or self.peer is not None
+        lr->grad only while nothing else has written it since the reduce that formed them: not
+        after an all-reduce of the gradient (RCCL / gloo / by hand at W > 1), and not after a
+        write declared with ``grad_written()``.  Otherwise the optimizer prologue forms
+        the norm from the gradient itself (the same summation order, so both give the same bits)."""
+        exact = (self.world_size == 1 or self.peer is not None) and not self._grad_dirty
         self.hp.flags = _lib.ADAM_F_NORM_PARTIALS if exact else 0
+
+    def grad_written(self):
+        """Declare a write to ``grad`` made outside the library's reduce (e.g. a hand-made
+        all-reduce or a test's injected gradient): the next optimizer step then forms the clip
+        norm from ``grad`` instead of the reduce's partials, which describe the overwritten
+        values.  The next reduce launch (swarm_reduce_advance / swarm_grad_reduce) clears it."""
+        self._grad_dirty = True
 
     def allreduce_grad(self):
         g = self.grad[:N_PARAMS + 1]   # parameters + loss sum (not the norm partials)
@@ -313,6 +327,7 @@ class SwarmEngine:
                                      ptr(self.slabs), stream_ptr()), "swarm_td_grad")
 
     def launch_grad_reduce(self):
+        self._grad_dirty = False
         check(self.lib.swarm_grad_reduce(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),
                                          ptr(self.grad), stream_ptr()), "swarm_grad_reduce")
 
@@ -326,6 +341,7 @@ class SwarmEngine:
 
     def launch_reduce_advance(self):
         """Slab reduce + ctrl advance; with a peer exchange, the gradient all-reduce too."""
+        self._grad_dirty = False
         if self.peer is not None:
             self.peer.check_stream()
             check(self.lib.swarm_reduce_advance_peer(ctypes_ref(self.cfg), ctypes_ref(self.hp), ptr(self.slabs),

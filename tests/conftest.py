@@ -9,6 +9,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# agent counts of the recorded evaluation runs committed as fixtures (tests/golden/make_golden.py):
+# every N the reference recorded, i.e. C5's whole 5-12 sweep (VERDICT r5 "next" #1)
+RECORDED_AGENTS = tuple(range(5, 13))
 # achieved errors of every numeric comparison, written at session end (record the
 # observed margins, not just pass/fail) to gpurun_out/parity_errors.<kind>.json, kind = "gpu" when
 # the session ran a test marked gpu, else "cpu": a CPU run never overwrites a GPU run's margins.

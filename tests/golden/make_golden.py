@@ -38,7 +38,7 @@ from oracle import swarm_oracle as O  # noqa: E402
 REF = "/root/reference/data"
 SCEN = [("go_to", O.SCENARIO_GOTO, "GoTo"), ("obstacle_avoidance", O.SCENARIO_OA, "ObstacleAvoidance")]
 SEEDS = (0, 4)
-AGENTS = (5, 8, 12)
+AGENTS = tuple(range(5, 13))   # every agent count the reference recorded (C5 sweeps 5-12)
 EPISODES = 8
 LEVEL_IDX = {0: 0, -1: 1, 1: 2}
 

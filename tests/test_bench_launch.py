@@ -62,3 +62,53 @@ def test_spawn_ranks_relays_and_checks(tmp_path, capsys, mode, want):
     lines = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
     assert len(lines) == 1 and lines[0]["args"] == [mode]   # rank 0's line, relayed once
     assert "progress text" in out
+
+
+HANG_SCRIPT = """
+import os, sys, time
+with open(os.path.join(sys.argv[1], "pid%s" % os.environ["RANK"]), "w") as f:
+    f.write(str(os.getpid()))
+time.sleep(600)
+"""
+
+RELAY = """
+import sys
+sys.path.insert(0, %r)
+import bench
+sys.exit(bench.spawn_ranks([%r], 2, script=%r))
+"""
+
+
+def test_sigterm_to_the_relay_stops_the_ranks(tmp_path):
+    """the rank launcher runs in its own session, so a SIGTERM to the relaying bench.py
+    (timeout(1), a harness) must still end the ranks: the relay's handler turns it into
+    SystemExit and its finally block terminates the launcher's process group."""
+    import signal
+    import subprocess
+    import time
+    script = tmp_path / "hang.py"
+    script.write_text(HANG_SCRIPT)
+    relay = subprocess.Popen([sys.executable, "-c", RELAY % (ROOT, str(tmp_path), str(script))])
+    pids = []
+    t0 = time.time()
+    while len(pids) < 2 and time.time() - t0 < 120:
+        pids = [int((tmp_path / f"pid{r}").read_text()) for r in range(2) if (tmp_path / f"pid{r}").exists()
+                and (tmp_path / f"pid{r}").read_text()]
+        time.sleep(0.2)
+    assert len(pids) == 2, "ranks did not start"
+    relay.send_signal(signal.SIGTERM)
+    assert relay.wait(timeout=60) != 0
+    deadline = time.time() + 30
+    alive = pids
+    while alive and time.time() < deadline:
+        alive = []
+        for p in pids:
+            try:
+                os.kill(p, 0)
+                alive.append(p)
+            except ProcessLookupError:
+                pass
+        time.sleep(0.2)
+    for p in alive:   # clean up before failing
+        os.kill(p, signal.SIGKILL)
+    assert not alive, f"ranks {alive} outlived the relay"

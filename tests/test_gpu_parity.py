@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from oracle import swarm_oracle as O
-from tests.conftest import assert_close_rel, assert_close_ulp, record
+from tests.conftest import RECORDED_AGENTS, assert_close_rel, assert_close_ulp, record
 
 # Tolerances in fp32 ulps of max(|reference|, 1), set from the achieved errors of the round-3
 # suite (profiles/r03_parity_errors.json: Q <= 19 ulp over 83 cases, TD loss <= 3.7 ulp); the
@@ -299,7 +299,7 @@ def test_gpu_reproduces_recorded_reference_actions(sw, golden_weights, trajector
     for seed in (0, 4):
         model = sw.GCN(7, 32, 9)
         model.load_state_dict(O.unflatten_params(_params(golden_weights, scen, seed)))
-        for n in (5, 8, 12):
+        for n in RECORDED_AGENTS:
             xs, refs = [], []
             for ep in range(8):
                 key = f"{scen}/s{seed}/n{n}/e{ep}"
@@ -836,6 +836,38 @@ def test_two_rank_fused_tick_equals_union_batch(sw, golden_weights):
     assert ra.read_ctrl()["adam_step"] == u.read_ctrl()["adam_step"] == 2
 
 
+@pytest.mark.parametrize("scen,N,B", [("GoTo", 8, 64), ("ObstacleAvoidance", 12, 64), ("ObstacleAvoidance", 5, 96)])
+def test_norm_partials_equal_the_prologue_norm(sw, golden_weights, scen, N, B):
+    """at W = 1 the fused tick's optimizer prologue takes the clip norm from the slab
+    reduce's partials (ADAM_F_NORM_PARTIALS); after a write declared with ``grad_written()`` it forms
+    the norm from grad itself.  Both are the one summation order of swarm_adam.h, so the same ticks
+    with flags 1 (engine a) and flags 0 (engine b) give bit-identical weights, moments, target and
+    control blocks (a sync every 2 ticks included)."""
+    from swarm_amd import _lib
+    key = "go_to" if scen == "GoTo" else "obstacle_avoidance"
+    kw = dict(seed=9, params=_params(golden_weights, key, 2), eps=0.2, batch=B, replay_capacity=4 * B,
+              update_target_every=2)
+    a, b = sw.SwarmEngine(scen, N, B, **kw), sw.SwarmEngine(scen, N, B, **kw)
+    assert a.fused and b.fused
+    for e in (a, b):
+        e.reset(0)
+        for _ in range(2):
+            e.act(push=True, full_out=False)
+            e.advance()
+    for t in range(5):
+        a.train_tick()
+        assert a.hp.flags == _lib.ADAM_F_NORM_PARTIALS
+        b.grad_written()
+        b.train_tick()
+        assert b.hp.flags == 0
+    for e in (a, b):
+        e.flush()
+    torch.cuda.synchronize()
+    for k in ("params", "adam_m", "adam_v", "target", "ctrl"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert a.read_ctrl()["adam_step"] >= 4
+
+
 def test_graph_capture_replay_equals_eager(sw, golden_weights):
     p = _params(golden_weights, "go_to", 1)
     a = sw.SwarmEngine("GoTo", 8, 128, seed=8, params=p, batch=128, eps=0.1)
@@ -1161,7 +1193,7 @@ def _recorded_action(pos, vel, P_next, sid):
 @pytest.mark.parametrize("scen", ["go_to", "obstacle_avoidance"])
 def test_closed_loop_rollout_reproduces_recorded_episodes(sw, golden_weights, trajectories, scen):
     """VERDICT r3 "next" #8: every recorded evaluation episode (tests/golden: model seeds 0 and 4,
-    5 / 8 / 12 agents, 8 episodes each) run by the closed-loop swarm_rollout launch (the
+    5 to 12 agents, 8 episodes each) run by the closed-loop swarm_rollout launch (the
     Simulator's path, simulator.py:47-109, kNN-5, argmax) from its own reset formation, recovered
     from the first two recorded steps (O.reset_from_first_step; the oracle's closed loop from the
     same starts reproduces every recorded tick bit for bit, tests/test_oracle_golden.py).
@@ -1176,7 +1208,7 @@ def test_closed_loop_rollout_reproduces_recorded_episodes(sw, golden_weights, tr
     for seed in (0, 4):
         p = _params(golden_weights, scen, seed)
         w = O.unflatten_params(p)
-        for n in (5, 8, 12):
+        for n in RECORDED_AGENTS:
             res = trajectories[f"{scen}/s{seed}/n{n}/result"]
             P = torch.tensor(np.stack([trajectories[f"{scen}/s{seed}/n{n}/e{e}/pos"] for e in range(8)]))
             T = P.shape[1]
@@ -1226,4 +1258,4 @@ def test_closed_loop_rollout_reproduces_recorded_episodes(sw, golden_weights, tr
                 assert bool((gap[diff].abs() <= 1e-4).all()), (seed, n, e, t, gap[diff])
                 counts["left_after_near_tie"] += 1
     record(f"{scen}: recorded evaluation episodes, closed loop from the recorded starts", counts)
-    assert counts["episodes"] == 48
+    assert counts["episodes"] == 16 * len(RECORDED_AGENTS)

@@ -1,7 +1,7 @@
 """The acting half against the oracle at the benchmarked sizes (VERDICT r3 "next" #2).
 
 C2 = GoTo, 8 agents x 1024 envs, GAT; C3 = ObstacleAvoidance, 12 agents x 1024 envs, GAT;
-C5's shard = ObstacleAvoidance, 5 and 12 agents x 512 envs per GPU, GAT and the a13 GCNConv
+C5's shard = ObstacleAvoidance, every N of the 5-12 sweep x 512 envs per GPU, GAT and the a13 GCNConv
 variant.  The fused training tick (swarm_train_tick + swarm_reduce_advance, the bench's launch) runs
 from a reset formation for four ticks with eps = 0.3, and every tick is compared with the oracle's
 act_tick (train_gcn_dqn.py:161-172: complete graph -> GCN.forward -> eps-greedy -> env.step), on the
@@ -28,6 +28,8 @@ pytestmark = pytest.mark.gpu
 CASES = [("C2", "GoTo", 8, 1024, "gat"), ("C3", "ObstacleAvoidance", 12, 1024, "gat"),
          ("C5 N=5 GAT", "ObstacleAvoidance", 5, 512, "gat"), ("C5 N=12 GAT", "ObstacleAvoidance", 12, 512, "gat"),
          ("C5 N=5 GCN", "ObstacleAvoidance", 5, 512, "gcn"), ("C5 N=12 GCN", "ObstacleAvoidance", 12, 512, "gcn")]
+# C5's sweep interior (VERDICT r5 "next" #1): every agent count from 5 to 12, GAT and GCN
+CASES += [(f"C5 N={n} {conv.upper()}", "ObstacleAvoidance", n, 512, conv) for n in (6, 7, 9, 10, 11) for conv in ("gat", "gcn")]
 SCEN = {"GoTo": O.SCENARIO_GOTO, "ObstacleAvoidance": O.SCENARIO_OA}
 EPS, SEED = 0.3, 21
 

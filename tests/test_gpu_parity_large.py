@@ -2,7 +2,7 @@
 
 C2 = GoTo, 8 agents x 1024 envs, TD batch S = 1024 graphs (256 TD blocks, 256 gradient slabs
 summed by the 105-block reduce); C3 = ObstacleAvoidance, 12 agents x 1024 envs, S = 1024 (one
-graph per TD wave); C5's shard = ObstacleAvoidance, 5 and 12 agents x 512 envs per GPU, S = 512,
+graph per TD wave); C5's shard = ObstacleAvoidance, every N of the 5-12 sweep x 512 envs per GPU, S = 512,
 GAT and the a13 GCNConv variant.  Both the reference-shaped API sequence (swarm_td_grad ->
 swarm_grad_reduce -> swarm_adam_step, train_gcn_dqn.py:112-137) and the headline's fused
 swarm_train_tick (whose TD graphs partly come from the tick's own replay slot through the
@@ -43,6 +43,10 @@ pytestmark = pytest.mark.gpu
 CASES = [("C2", "GoTo", 8, 1024, 1024, "gat"), ("C3", "ObstacleAvoidance", 12, 1024, 1024, "gat"),
          ("C5 N=5 GAT", "ObstacleAvoidance", 5, 512, 512, "gat"), ("C5 N=12 GAT", "ObstacleAvoidance", 12, 512, 512, "gat"),
          ("C5 N=5 GCN", "ObstacleAvoidance", 5, 512, 512, "gcn"), ("C5 N=12 GCN", "ObstacleAvoidance", 12, 512, 512, "gcn")]
+# C5's sweep interior (VERDICT r5 "next" #1): N = 6, 7 run the 8-slot kernels with 2 / 1 padded
+# slots, N = 9, 10, 11 the 16-slot kernels with 7 / 6 / 5 padded slots (N = 12 has 4)
+CASES += [(f"C5 N={n} {conv.upper()}", "ObstacleAvoidance", n, 512, 512, conv)
+          for n in (6, 7, 9, 10, 11) for conv in ("gat", "gcn")]
 SCEN = {"GoTo": O.SCENARIO_GOTO, "ObstacleAvoidance": O.SCENARIO_OA}
 
 
