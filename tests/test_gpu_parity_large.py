@@ -30,7 +30,9 @@ parity_errors.gpu.json via conftest.record and are kept under profiles/):
 - Adam, isolated from the gradient: m, v and the weights against torch.optim.Adam applied to the
   GPU's OWN gradient: m within 8 ulps and v within 16 ulps of the magnitude of their update terms
   (beta * old + (1 - beta) * new), the weights within 4 ulps of max(|w|, lr);
-- end to end, weights after Adam within 2e-6 of torch's update on the fp32 oracle's gradient.
+- end to end, weights after Adam within 2e-6 of torch's update on the fp32 oracle's gradient, plus,
+  per element, the difference Adam itself makes of the two gradients' difference (round 6: near
+  Adam's eps the update amplifies last-bit gradient differences; _end_to_end_weights).
 """
 import pytest
 import torch
@@ -202,13 +204,38 @@ def _compare_update(name, eng, p0, t0, idx, S, N, scen, conv):
     return g32s[0], grad[:O.N_PARAMS].clone()
 
 
-def _end_to_end_weights(name, p_gpu, p0, g32, m0, v0, step0):
-    """weights after Adam vs torch's update on the fp32 oracle's gradient (2e-6 absolute)."""
+def _clip_adam64(p0, g, m0, v0, step0, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, max_norm=1.0):
+    """clip_grad_norm_ + one torch.optim.Adam step (train_gcn_dqn.py:85,125-126), in float64."""
+    p0, g = p0.double(), g.double()
+    m0 = torch.zeros_like(p0) if m0 is None else m0.double()
+    v0 = torch.zeros_like(p0) if v0 is None else v0.double()
+    coef = min(1.0, max_norm / (float(g.norm()) + 1e-6))
+    gc = g * coef
+    m, v, t = b1 * m0 + (1 - b1) * gc, b2 * v0 + (1 - b2) * gc * gc, step0 + 1
+    return p0 - (lr / (1 - b1 ** t)) * m / ((v / (1 - b2 ** t)).sqrt() + eps)
+
+
+def _end_to_end_weights(name, p_gpu, p0, g32, m0, v0, step0, g_gpu=None):
+    """weights after Adam vs torch's update on the fp32 oracle's gradient: within 2e-6, plus, per
+    element, the difference that Adam itself makes of the two gradients' difference (both updates in
+    float64).  Adam normalises each element by sqrt(v) + eps, so where a clipped gradient element is
+    near eps = 1e-8 the update moves by up to lr * |dg| / (4 eps): the first C5 N = 6 fused tick has
+    such an element, where the two fp32 gradients' last-bit difference (both within the gradient
+    bounds of _grad_bound_check) became 1.1e-5 of weight.  Adam's own arithmetic is checked apart
+    from the gradient, in ulps, by _adam_check."""
     ref_p, _, _, ref_norm = O.clip_adam(p0, g32, torch.zeros_like(p0) if m0 is None else m0,
                                         torch.zeros_like(p0) if v0 is None else v0, step0)
     st = error_stats(p_gpu, ref_p)
+    allow = torch.full_like(p_gpu, 2e-6, dtype=torch.float64)
+    if g_gpu is not None:
+        sens = (_clip_adam64(p0, g_gpu, m0, v0, step0) - _clip_adam64(p0, g32, m0, v0, step0)).abs()
+        allow = allow + sens
+        st["elements_over_2e-6_explained_by_the_gradient_difference"] = int(
+            ((p_gpu.double() - ref_p.double()).abs() > 2e-6).sum())
+    ratio = float(((p_gpu.double() - ref_p.double()).abs() / allow).max())
+    st["largest_error_over_allowance"] = ratio
     record(f"{name} weights after Adam vs the oracle-gradient update", st)
-    assert st["max_abs"] < 2e-6, st
+    assert ratio <= 1.0, st
     return ref_norm
 
 
@@ -232,7 +259,7 @@ def test_td_api_update_at_benchmark_size(sw, golden_weights, name, scen, N, B, S
     torch.cuda.synchronize()
     c = eng.read_ctrl()
     assert c["adam_step"] == 1
-    ref_norm = _end_to_end_weights(name, eng.params.cpu(), p0, g32, None, None, 0)
+    ref_norm = _end_to_end_weights(name, eng.params.cpu(), p0, g32, None, None, 0, g_gpu=g_gpu)
     assert ref_norm > 1.0, "the clip must be active at these sizes (norm > max_norm)"
     assert_close_rel(c["grad_norm"], ref_norm, 1e-5, f"{name} clip total_norm")
     _adam_check(name, eng.params.cpu(), eng.adam_m.cpu(), eng.adam_v.cpu(), p0, g_gpu, None, None, 0,
@@ -264,7 +291,7 @@ def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, 
         p_used, m_used, v_used = eng.params.cpu().clone(), eng.adam_m.cpu().clone(), eng.adam_v.cpu().clone()
         if prev is not None:
             pw, g32p, ggp, mp, vp, sp = prev
-            _end_to_end_weights(f"{name} fused tick {t}", p_used, pw, g32p, mp, vp, sp)
+            _end_to_end_weights(f"{name} fused tick {t}", p_used, pw, g32p, mp, vp, sp, g_gpu=ggp)
             _adam_check(f"{name} fused tick {t}", p_used, m_used, v_used, pw, ggp, mp, vp, sp)
         idx = eng.samples.cpu().clone()
         assert len(set(idx.tolist())) == S
@@ -276,7 +303,7 @@ def test_fused_tick_update_at_benchmark_size(sw, golden_weights, name, scen, N, 
     eng.flush()
     torch.cuda.synchronize()
     pw, g32p, ggp, mp, vp, sp = prev
-    _end_to_end_weights(f"{name} fused flushed second step", eng.params.cpu(), pw, g32p, mp, vp, sp)
+    _end_to_end_weights(f"{name} fused flushed second step", eng.params.cpu(), pw, g32p, mp, vp, sp, g_gpu=ggp)
     _adam_check(f"{name} fused flushed second step", eng.params.cpu(), eng.adam_m.cpu(), eng.adam_v.cpu(), pw, ggp,
                 mp, vp, sp)
 
@@ -310,7 +337,7 @@ def test_fused_tick_target_sync_at_benchmark_size(sw, golden_weights):
     assert eng.handoff_errors() == 0
     w4, tgt4 = eng.params.cpu().clone(), eng.target.cpu().clone()
     assert not torch.equal(w4, p3) and torch.equal(tgt4, w4), "the target row is the post-step weights"
-    _end_to_end_weights(f"{name} synced target", tgt4, p3, g32, None, None, 0)
+    _end_to_end_weights(f"{name} synced target", tgt4, p3, g32, None, None, 0, g_gpu=g_gpu)
     _adam_check(f"{name} synced target", tgt4, eng.adam_m.cpu(), eng.adam_v.cpu(), p3, g_gpu, None, None, 0)
     _compare_update(f"{name} tick 4 (synced target)", eng, w4, tgt4, eng.samples.cpu().clone(), S, N, scen, conv)
     # tick 5: step applied, no sync (5 % 2 != 0)
