@@ -673,10 +673,18 @@ def cpu_baseline_leg(args, w0, scen, B, N, S, eng):
                                       "sample": "40 episodes, reset + one 50-tick swarm_rollout launch each"}}}
 
 
+ACT_PMC_CONFIG = ("GoTo", 8, 1024, "knn", 5, "gat", "gcn")   # the acting line whose rollout has PMC passes
+
+
 def rollout_roofline(args, eng, max_steps, f_node):
     """The rollout kernel's roofline: algorithmic FLOPs of one max_steps-tick swarm_rollout launch
     (B·N·ticks·(forward + ≈300 FLOP of physics)) ÷ that launch's duration, HIP events on its stream
-    (median of 5 launches), against the FP32 peak."""
+    (median of 5 launches), against the FP32 peak.  For the headline acting configuration (GoTo
+    8 x 1024, kNN-5) `traffic` is the launch's HBM bytes from the PMC summary of THIS build
+    (tools/pmc_summary.py, kernel "rollout"), beside SURVEY §8(d)'s algorithmic 56 B per
+    agent-step (state 32 + replay push 24) and the rollout's own minimum (the state read and
+    written once per launch: it stays in registers across the ticks, and a rollout pushes no
+    replay)."""
     B, N = args.envs, args.agents
     stream = torch.cuda.current_stream()
     per = []
@@ -691,10 +699,22 @@ def rollout_roofline(args, eng, max_steps, f_node):
     t_l = float(np.median(per))
     flops = B * N * max_steps * f_node
     ach = flops / t_l / 1e12
+    traffic, pmc = None, {"file": None, "reason": "counters are collected for the headline acting configuration only"}
+    if (args.scenario, N, B, args.graph, args.knn_k, args.conv, args.net) == ACT_PMC_CONFIG:
+        pmc = find_pmc("rollout", lib_identity())
+        if pmc.get("file"):
+            traffic = pmc.pop("data").get("hbm_bytes_per_launch")
+    alg_bytes = 56 * B * N * max_steps
     return {"bound": "valu" if args.net == "gat3" else "mfma", "achieved": round(ach, 4),
-            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": None,
+            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": traffic,
             "kernel": "act_kernel rollout (swarm_rollout)", "algorithmic_flops_per_launch": flops,
-            "flops_per_agent_step": f_node, "launch_us": round(t_l * 1e6, 2)}
+            "flops_per_agent_step": f_node, "launch_us": round(t_l * 1e6, 2),
+            "algorithmic_bytes_per_launch": alg_bytes,
+            # state read + written once (32 B per agent), reward sums (4) and last obs (24) per agent,
+            # mean goal distance and hits per env (8)
+            "rollout_minimum_bytes_per_launch": 60 * B * N + 8 * B,
+            "traffic_over_algorithmic": (traffic / alg_bytes) if traffic else None,
+            "hbm_gbs": round(traffic / t_l / 1e9, 2) if traffic else None, "pmc": pmc}
 
 
 def acting_fnode(args, eng) -> float:
@@ -770,7 +790,7 @@ def bench_act(args, eng, world, rank, distributed, max_steps):
                                        f"{g} graph, eps 0, frozen weights", "envs_per_gpu": B, "agents": N,
                            "global_envs": B * world, "graph": args.graph, "conv": args.conv,
                            "parallelism": f"replicas x{world}"},
-                "roofline": roof, "cpu_baseline": None}
+                "roofline": roof, "cpu_baseline": None, "build": lib_identity()}
         print(json.dumps(line))
     if distributed:
         torch.distributed.destroy_process_group()

@@ -401,6 +401,9 @@ static int reduce_advance(const swarm_config* cfg, const swarm_adam_cfg* hp, con
   ReduceArgs a = {};
   if (peer) a.peer = *peer;
   a.n_slabs = td_blocks(cfg, hp->batch); a.slabs = slabs; a.grad = lr->grad;
+#if SWARM_DIAG_FEWSLABS   // diagnostic builds only: the reduce reads K slabs (timing bound of a slab cut)
+  a.n_slabs = a.n_slabs < SWARM_DIAG_FEWSLABS ? a.n_slabs : SWARM_DIAG_FEWSLABS;
+#endif
   a.advance = 1; a.lr = *lr; a.ctrl = ctrl;
   a.capacity = replay_capacity; a.B = cfg->n_envs; a.N = cfg->n_agents; a.batch = hp->batch;
   a.hp = *hp;

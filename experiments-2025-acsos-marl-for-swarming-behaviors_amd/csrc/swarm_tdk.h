@@ -77,6 +77,9 @@ struct TdArgs {
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
 // measured against nt (td 8.4 vs 8.0 us) and write-through sc1 (9.5 us) stores.
 __device__ inline void slab_st(float* p, float v) { *p = v; }
+#ifndef SWARM_DIAG_FEWSLABS
+#define SWARM_DIAG_FEWSLABS 0   // diagnostic builds only: > 0 = only the first K TD blocks store slabs (timing bound)
+#endif
 
 // NS node slots per wave holding NS / GS graphs of GS slots (GS = 8 < NS = 16 packs two
 // N <= 8 graphs into one wave: every MFMA column is a real node, one wave per SIMD).
@@ -179,7 +182,13 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   static_assert(kSlabCols == 16, "slab column blocks of 16");
   float* const slab_base = A.slabs + (size_t)vb * kSlabCols;
   const uint32_t slab_stride = (uint32_t)A.n_slabs * kSlabCols;
+#if SWARM_DIAG_FEWSLABS
+  auto sst = [&](int q, float v) {
+    if (vb < SWARM_DIAG_FEWSLABS) slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v);
+  };
+#else
   auto sst = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
+#endif
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
@@ -318,6 +327,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   bool pre = false;
 #pragma unroll
   for (int w2 = 0; w2 < GPB; ++w2) pre = pre || TB.insl[w2] != 0;
+#if SWARM_DIAG_PRE_ALL   // diagnostic builds only (tools/ab_build.py): every block on the pre path
+  pre = true;
+#endif
   pre = pre && online;
   const uint32_t tag = cc.tick + 1u;
   // granule address of this lane's node in a hand-off record: s at 0, s' at 4N, r at 8N, a at 9N

@@ -19,7 +19,10 @@ import os
 import statistics
 import sys
 
-KERNELS = {"tick": "tick_kernel", "td": "td_kernel", "act": "act_kernel<8, 1>", "reduce": "grad_reduce_kernel"}
+# "rollout": the acting-only line's kernel, the kNN + GAT specialised rollout of GoTo 8 x 1024 with
+# k = 5 (bench.py --mode act --graph knn --knn-k 5; the headline acting_only line)
+KERNELS = {"tick": "tick_kernel", "td": "td_kernel", "act": "act_kernel<8, 1>", "reduce": "grad_reduce_kernel",
+           "rollout": "act_kernel<8, 2, 0, 3, 0>"}
 
 
 def pass_builds(src):
@@ -70,7 +73,8 @@ def main(src, dst):
             # MFMA pipe cycles over every SIMD's cycles while the GPU was busy with the dispatch:
             # GRBM_GUI_ACTIVE sums the 8 XCDs, each with 128 SIMDs (reads high on short dispatches)
             out["kernels"][key]["mfma_busy_frac_grbm"] = k["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * k["GRBM_GUI_ACTIVE"])
-    main_k = "tick" if "tick" in out["kernels"] else "td"   # the bench line's dominant kernel
+    # the bench line's dominant kernel: training lines the tick (or TD) kernel, acting lines the rollout
+    main_k = next((k for k in ("tick", "td", "rollout") if k in out["kernels"]), "td")
     if main_k in out["kernels"]:
         out["kernel"] = main_k
         out["hbm_bytes_per_launch"] = out["kernels"][main_k]["hbm_bytes_per_launch"]

@@ -10,8 +10,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["SWARM_LIB_PATH"] = os.path.join(ROOT, "experiments-2025-acsos-marl-for-swarming-behaviors_amd",
-                                            "libswarm_hip_stamps.so")
+# SWARM_TL_LIB: a prebuilt stamps library to run instead (e.g. a diagnostic variant from
+# tools/ab_build.py with -DSWARM_STAMPS=1); the in-tree stamps build otherwise
+TL_LIB = os.environ.get("SWARM_TL_LIB")
+os.environ["SWARM_LIB_PATH"] = TL_LIB or os.path.join(ROOT, "experiments-2025-acsos-marl-for-swarming-behaviors_amd",
+                                                      "libswarm_hip_stamps.so")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -30,7 +33,8 @@ TD_WAIT_ORDER = [0, 1, 2, 16, 17, 18, 19, 20, 3, 4, 5, 25, 27, 26, 6, 7]
 
 def main():
     from swarm_amd import build as swbuild
-    swbuild.build(stamps=True)
+    if not TL_LIB:
+        swbuild.build(stamps=True)
     lib = _lib.load()
     raw = ctypes.CDLL(_lib.LIB_PATH)
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
