@@ -77,6 +77,26 @@ struct TdArgs {
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
 // measured against nt (td 8.4 vs 8.0 us) and write-through sc1 (9.5 us) stores.
 __device__ inline void slab_st(float* p, float v) { *p = v; }
+// SWARM_SLAB_MODE: how a TD block's slab reaches global memory.
+//   0: each element stored (plain 4-B store) where its job forms it;
+//   1: the elements are staged in LDS and the block stores the slab as 16-B write-through (sc1)
+//      stores after one block barrier: the lines leave the XCD's L2 as they are written, so the
+//      launch ends without a dirty slab write-back (MI355X_MICROARCH.md "boundary": + B / 6 TB/s),
+//      and a 16-B sc1 store costs what a plain one does (4-B sc1 stores cost ~6x per byte);
+//   2: staged, 16-B plain stores;  3: staged, 16-B nt stores.
+#ifndef SWARM_SLAB_MODE
+#define SWARM_SLAB_MODE 0
+#endif
+typedef float slab_f4 __attribute__((ext_vector_type(4)));
+__device__ inline void slab_st4(float* p, slab_f4 v) {
+#if SWARM_SLAB_MODE == 1
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#elif SWARM_SLAB_MODE == 3
+  __builtin_nontemporal_store(v, reinterpret_cast<slab_f4*>(p));
+#else
+  *reinterpret_cast<slab_f4*>(p) = v;
+#endif
+}
 #ifndef SWARM_DIAG_FEWSLABS
 #define SWARM_DIAG_FEWSLABS 0   // diagnostic builds only: > 0 = only the first K TD blocks store slabs (timing bound)
 #endif
@@ -183,11 +203,19 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   float* const slab_base = A.slabs + (size_t)vb * kSlabCols;
   const uint32_t slab_stride = (uint32_t)A.n_slabs * kSlabCols;
 #if SWARM_DIAG_FEWSLABS
-  auto sst = [&](int q, float v) {
+  auto sst_g = [&](int q, float v) {
     if (vb < SWARM_DIAG_FEWSLABS) slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v);
   };
 #else
-  auto sst = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
+  auto sst_g = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
+#endif
+#if SWARM_SLAB_MODE
+  // the slab image: the target weights' LDS image, free once the block passed B1 (the target
+  // waves' forwards were its last readers); every slab element is written after B2
+  float* const slab_img = L.Ptg;
+  auto sst = [&](int q, float v) { slab_img[q] = v; };
+#else
+  auto sst = sst_g;
 #endif
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
@@ -278,7 +306,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   }
   // ---- skip while the replay holds fewer than `batch` graphs (train_gcn_dqn.py:113-115)
   if (n_graphs < (uint32_t)S) {
-    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) sst(q, 0.0f);
+    for (int q = threadIdx.x; q <= N_PARAMS; q += NT) sst_g(q, 0.0f);
     return;
   }
   if (sample_out && online && p == 0) {
@@ -904,6 +932,15 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
   }
+#if SWARM_SLAB_MODE
+  __syncthreads();   // B4: the block's slab image is complete
+  // 16-column runs of 64 B (column-block-major slab_index): quad i = columns 4i..4i+3 of column
+  // block i / 4; the run's padding columns (1674..1679) carry whatever the image holds there and
+  // are never read (the reduce reads columns <= N_PARAMS)
+  for (int i = threadIdx.x; i < kSlabQuads; i += NT)
+    slab_st4(slab_base + ((uint32_t)(i >> 2) * slab_stride + (uint32_t)((i & 3) * 4)),
+             reinterpret_cast<const slab_f4*>(slab_img)[i]);
+#endif
   SWARM_STAMP(7);
   SWARM_RTSTAMP(9);
 }
