@@ -358,6 +358,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #if SWARM_DIAG_PRE_ALL   // diagnostic builds only (tools/ab_build.py): every block on the pre path
   pre = true;
 #endif
+#if SWARM_PRE_WARM   // A/B knob: every SWARM_PRE_WARM-th TD block also takes the pre path (warms its code)
+  pre = pre || (vb % SWARM_PRE_WARM) == 0;
+#endif
   pre = pre && online;
   const uint32_t tag = cc.tick + 1u;
   // granule address of this lane's node in a hand-off record: s at 0, s' at 4N, r at 8N, a at 9N
