@@ -202,9 +202,14 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   static_assert(kSlabCols == 16, "slab column blocks of 16");
   float* const slab_base = A.slabs + (size_t)vb * kSlabCols;
   const uint32_t slab_stride = (uint32_t)A.n_slabs * kSlabCols;
-#if SWARM_DIAG_FEWSLABS
+#if SWARM_DIAG_FEWSLABS > 0
   auto sst_g = [&](int q, float v) {
     if (vb < SWARM_DIAG_FEWSLABS) slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v);
+  };
+#elif SWARM_DIAG_FEWSLABS < 0   // -1: blocks holding a graph of this tick's slot skip their stores; -2: the others do
+  bool diag_skip = false;   // set once the block knows whether it holds such a graph
+  auto sst_g = [&](int q, float v) {
+    if (!diag_skip) slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v);
   };
 #else
   auto sst_g = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
@@ -357,6 +362,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
   for (int w2 = 0; w2 < GPB; ++w2) pre = pre || TB.insl[w2] != 0;
 #if SWARM_DIAG_PRE_ALL   // diagnostic builds only (tools/ab_build.py): every block on the pre path
   pre = true;
+#endif
+#if SWARM_DIAG_FEWSLABS < 0
+  diag_skip = (SWARM_DIAG_FEWSLABS == -1) == pre;
 #endif
 #if SWARM_PRE_WARM   // A/B knob: every SWARM_PRE_WARM-th TD block also takes the pre path (warms its code)
   pre = pre || (vb % SWARM_PRE_WARM) == 0;
