@@ -214,6 +214,18 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #else
   auto sst_g = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
 #endif
+#if SWARM_B2_T   // 16-B stores of four consecutive parameters q .. q + 3 (q % 4 == 0, one slab run)
+  static_assert(OFF_W1 % 16 == 0 && OFF_W2 % 16 == 0 && kHidden % 16 == 0, "16-B slab pieces");
+  auto sst4 = [&](int q, f32x4 v) {
+    float* const ptr = slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15));
+    const slab_f4 x = {v[0], v[1], v[2], v[3]};
+#if SWARM_B2_T == 2
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(x) : "memory");
+#else
+    *reinterpret_cast<slab_f4*>(ptr) = x;
+#endif
+  };
+#endif
 #if SWARM_SLAB_MODE
   // the slab image: the target weights' LDS image, free once the block passed B1 (the target
   // waves' forwards were its last readers); every slab element is written after B2
@@ -691,6 +703,20 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
     for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
+#if SWARM_B2_T
+    // the transposed tiles (operands swapped: the same products, the same K order): lane (c, p)
+    // holds dW1[out = c (+16)][in = 16 tj + 4p .. 4p + 3] and dW2[action = c][in = ...], four
+    // consecutive parameters of one 16-column slab run, stored as ONE 16-B store per tile
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      d0 = mfma16(b1[s], a1[0][s], d0);
+      d1 = mfma16(b1[s], a1[1][s], d1);
+      d2 = mfma16(b2v[s], an[s] == c ? a2[s] : 0.0f, d2);
+    }
+    sst4(OFF_W1 + c * kHidden + 16 * tj + 4 * p, d0);
+    sst4(OFF_W1 + (16 + c) * kHidden + 16 * tj + 4 * p, d1);
+    if (c < kActions) sst4(OFF_W2 + c * kHidden + 16 * tj + 4 * p, d2);
+#else
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       d0 = mfma16(a1[0][s], b1[s], d0);
@@ -703,6 +729,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       sst(OFF_W1 + (16 + 4 * p + r) * kHidden + 16 * tj + c, d1[r]);
       if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
     }
+#endif
   };
   auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
     if (job == 2) {
