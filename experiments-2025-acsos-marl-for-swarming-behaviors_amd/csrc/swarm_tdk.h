@@ -220,7 +220,16 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     float* const ptr = slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15));
     const slab_f4 x = {v[0], v[1], v[2], v[3]};
 #if SWARM_B2_T == 2
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(x) : "memory");
+    // inline asm is invisible to the compiler's hazard recognizer: the store's data are MFMA
+    // results, which a vector-memory read may take only after the MFMA's wait states (not
+    // interlocked); without the padding the store read partial sums (tools/bitcmp.py)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tglobal_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(x) : "memory");
+#elif SWARM_B2_T == 3   // two compiler-generated 8-B write-through stores (agent-scope relaxed atomics)
+    typedef __attribute__((address_space(1))) unsigned long long g64;
+    const unsigned long long lo = ((unsigned long long)__float_as_uint(x[1]) << 32) | __float_as_uint(x[0]);
+    const unsigned long long hi = ((unsigned long long)__float_as_uint(x[3]) << 32) | __float_as_uint(x[2]);
+    __hip_atomic_store((g64*)ptr, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((g64*)(ptr + 2), hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
     *reinterpret_cast<slab_f4*>(ptr) = x;
 #endif
