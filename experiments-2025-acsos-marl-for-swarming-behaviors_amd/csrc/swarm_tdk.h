@@ -216,10 +216,16 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #endif
 #if SWARM_B2_T   // 16-B stores of four consecutive parameters q .. q + 3 (q % 4 == 0, one slab run)
   static_assert(OFF_W1 % 16 == 0 && OFF_W2 % 16 == 0 && kHidden % 16 == 0, "16-B slab pieces");
+  bool ho_block = false;   // the block holds a graph of this tick's slot (set with `pre` below)
   auto sst4 = [&](int q, f32x4 v) {
     float* const ptr = slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15));
     const slab_f4 x = {v[0], v[1], v[2], v[3]};
-#if SWARM_B2_T == 2
+#if SWARM_B2_T == 4   // write-through in blocks off the hand-off chain, plain in the blocks on it
+    if (!ho_block)
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tglobal_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(x) : "memory");
+    else
+      *reinterpret_cast<slab_f4*>(ptr) = x;
+#elif SWARM_B2_T == 2
     // inline asm is invisible to the compiler's hazard recognizer: the store's data are MFMA
     // results, which a vector-memory read may take only after the MFMA's wait states (not
     // interlocked); without the padding the store read partial sums (tools/bitcmp.py)
@@ -386,6 +392,9 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #endif
 #if SWARM_DIAG_FEWSLABS < 0
   diag_skip = (SWARM_DIAG_FEWSLABS == -1) == pre;
+#endif
+#if SWARM_B2_T
+  ho_block = pre;
 #endif
 #if SWARM_PRE_WARM   // A/B knob: every SWARM_PRE_WARM-th TD block also takes the pre path (warms its code)
   pre = pre || (vb % SWARM_PRE_WARM) == 0;

@@ -8,7 +8,7 @@ REPS=${REPS:-3}
 : > gpurun_out/ab.jsonl
 for rep in $(seq $REPS); do
   for v in $VARIANTS; do
-    if [ "$v" = base ]; then lib=""; else lib="$PWD/ab/libswarm_$v.so"; fi
+    if [ "$v" = base ]; then lib="$PWD/experiments-2025-acsos-marl-for-swarming-behaviors_amd/libswarm_hip.so"; else lib="$PWD/ab/libswarm_$v.so"; fi
     SWARM_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu-baseline $BENCH_ARGS > gpurun_out/ab_$v.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; tail -5 gpurun_out/ab_$v.log; exit $rc; fi
