@@ -76,7 +76,16 @@ struct TdArgs {
 
 // gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
 // measured against nt (td 8.4 vs 8.0 us) and write-through sc1 (9.5 us) stores.
-__device__ inline void slab_st(float* p, float v) { *p = v; }
+#ifndef SWARM_SLAB_WT_ALL
+#define SWARM_SLAB_WT_ALL 0   // A/B knob: the 4-B slab stores write-through too (agent-scope relaxed)
+#endif
+__device__ inline void slab_st(float* p, float v) {
+#if SWARM_SLAB_WT_ALL
+  __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
 // SWARM_SLAB_MODE: how a TD block's slab reaches global memory.
 //   0: each element stored (plain 4-B store) where its job forms it;
 //   1: the elements are staged in LDS and the block stores the slab as 16-B write-through (sc1)
