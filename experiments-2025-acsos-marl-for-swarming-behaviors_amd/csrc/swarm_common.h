@@ -201,6 +201,19 @@ __device__ inline unsigned long long ld_granule(const unsigned long long* g) {
   return __hip_atomic_load((const gran_t*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One 16-B write-through store (global_store_dwordx4 ... sc1): the line leaves the XCD's L2 as it
+// is written, so a launch that ends after it leaves no dirty line behind for the end-of-kernel
+// write-back (MI355X_MICROARCH.md "boundary": + bytes / 6 TB/s), and a 16-B sc1 store costs what a
+// plain one does.  Inline asm is invisible to the compiler's hazard recognizer: the data may be
+// MFMA results, which a vector-memory instruction may read only after the MFMA's wait states (not
+// interlocked; without the padding a store read partial sums, profiles/r06_bitcmp_b2t_v1.jsonl),
+// so 24 wait states lead the store.  Vector store only (never a scalar-cache write).
+__device__ inline void st16_wt(float* p, float a, float b, float c, float d) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v x = {a, b, c, d};
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tglobal_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+
 // ---------------------------------------------------------------- small math
 __host__ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * kLeakySlope; }
 

@@ -226,19 +226,15 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #if SWARM_B2_T   // 16-B stores of four consecutive parameters q .. q + 3 (q % 4 == 0, one slab run)
   static_assert(OFF_W1 % 16 == 0 && OFF_W2 % 16 == 0 && kHidden % 16 == 0, "16-B slab pieces");
   bool ho_block = false;   // the block holds a graph of this tick's slot (set with `pre` below)
+  (void)ho_block;
   auto sst4 = [&](int q, f32x4 v) {
     float* const ptr = slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15));
     const slab_f4 x = {v[0], v[1], v[2], v[3]};
 #if SWARM_B2_T == 4   // write-through in blocks off the hand-off chain, plain in the blocks on it
-    if (!ho_block)
-      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tglobal_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(x) : "memory");
-    else
-      *reinterpret_cast<slab_f4*>(ptr) = x;
+    if (!ho_block) st16_wt(ptr, x[0], x[1], x[2], x[3]);
+    else *reinterpret_cast<slab_f4*>(ptr) = x;
 #elif SWARM_B2_T == 2
-    // inline asm is invisible to the compiler's hazard recognizer: the store's data are MFMA
-    // results, which a vector-memory read may take only after the MFMA's wait states (not
-    // interlocked); without the padding the store read partial sums (tools/bitcmp.py)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\tglobal_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(x) : "memory");
+    st16_wt(ptr, x[0], x[1], x[2], x[3]);   // swarm_common.h: write-through, hazard-padded
 #elif SWARM_B2_T == 3   // two compiler-generated 8-B write-through stores (agent-scope relaxed atomics)
     typedef __attribute__((address_space(1))) unsigned long long g64;
     const unsigned long long lo = ((unsigned long long)__float_as_uint(x[1]) << 32) | __float_as_uint(x[0]);
