@@ -12,10 +12,6 @@
 #include "swarm_dl.h"
 #include "swarm_gat3.h"
 
-#ifndef SWARM_ACT_WT
-#define SWARM_ACT_WT 0   // A/B knob: the fused tick's replay push (s, s') and state stores write-through
-#endif
-
 namespace swarm {
 
 enum { MODE_Q = 0, MODE_TICK = 1, MODE_ROLLOUT = 2, MODE_STEP = 3 };
@@ -502,13 +498,8 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
             }
           } else if (MODE == MODE_TICK && rp_s) {
             const size_t ri = ((size_t)slot * B + d.gid) * N + n;
-#if SWARM_ACT_WT   // the replay rows write-through (swarm_common.h st16_wt): no dirty lines at the launch end
-            if (p == 1) st16_wt(rp_s + 4 * ri, px[ct], py[ct], vx[ct], vy[ct]);
-            else if (p == 2) st16_wt(rp_sn + 4 * ri, o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
-#else
             if (p == 1) reinterpret_cast<float4*>(rp_s)[ri] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
             else if (p == 2) reinterpret_cast<float4*>(rp_sn)[ri] = make_float4(o[ct].px, o[ct].py, o[ct].vx, o[ct].vy);
-#endif
             else { rp_r[ri] = rew; rp_a[ri] = (uint8_t)action[ct]; }
           }
           if (p == 3 && A.out.obs) {
@@ -547,12 +538,7 @@ __device__ __forceinline__ void act_body(ActSmem<NS>& S, const int vb, const int
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     if (valid[ct] && p == 0) {
-#if SWARM_ACT_WT
-      if (MODE == MODE_TICK) st16_wt(state + 4 * node[ct], px[ct], py[ct], vx[ct], vy[ct]);
-      else reinterpret_cast<float4*>(state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
-#else
       reinterpret_cast<float4*>(state)[node[ct]] = make_float4(px[ct], py[ct], vx[ct], vy[ct]);
-#endif
       if (fl_prev) fl_prev[node[ct]] = spread[ct];
       if (MODE == MODE_ROLLOUT) {
         if (A.out.reward) A.out.reward[node[ct]] = rew_sum[ct];

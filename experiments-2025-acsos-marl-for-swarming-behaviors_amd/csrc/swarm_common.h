@@ -170,8 +170,6 @@ __host__ __device__ inline uint32_t sample_position(uint32_t g, const SampleKey&
 // 64-B piece of every 6.7-KB slab row.
 constexpr int kSlabCols = 16;
 constexpr int kSlabColBlocks = (N_PARAMS + 1 + kSlabCols - 1) / kSlabCols;
-constexpr int kSlabQuads = kSlabColBlocks * kSlabCols / 4;   // 16-B pieces of one block's slab
-static_assert(kSlabColBlocks * kSlabCols <= N_LDS_PARAMS, "a slab fits the LDS weight image it is staged in");
 __host__ __device__ constexpr size_t slab_floats_per_block() { return (size_t)kSlabColBlocks * kSlabCols; }
 __host__ __device__ inline size_t slab_index(int q, int b, int n_slabs) {
   return ((size_t)(q / kSlabCols) * n_slabs + b) * kSlabCols + (q % kSlabCols);

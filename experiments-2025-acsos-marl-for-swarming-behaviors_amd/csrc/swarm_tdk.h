@@ -74,38 +74,10 @@ struct TdArgs {
   int n_slabs;        // TD blocks of the launch (slab layout, swarm_common.h slab_index)
 };
 
-// gradient-slab store (read once by the next launch, from another XCD).  Plain stores:
-// measured against nt (td 8.4 vs 8.0 us) and write-through sc1 (9.5 us) stores.
-#ifndef SWARM_SLAB_WT_ALL
-#define SWARM_SLAB_WT_ALL 0   // A/B knob: the 4-B slab stores write-through too (agent-scope relaxed)
-#endif
-__device__ inline void slab_st(float* p, float v) {
-#if SWARM_SLAB_WT_ALL
-  __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
-}
-// SWARM_SLAB_MODE: how a TD block's slab reaches global memory.
-//   0: each element stored (plain 4-B store) where its job forms it;
-//   1: the elements are staged in LDS and the block stores the slab as 16-B write-through (sc1)
-//      stores after one block barrier: the lines leave the XCD's L2 as they are written, so the
-//      launch ends without a dirty slab write-back (MI355X_MICROARCH.md "boundary": + B / 6 TB/s),
-//      and a 16-B sc1 store costs what a plain one does (4-B sc1 stores cost ~6x per byte);
-//   2: staged, 16-B plain stores;  3: staged, 16-B nt stores.
-#ifndef SWARM_SLAB_MODE
-#define SWARM_SLAB_MODE 0
-#endif
-typedef float slab_f4 __attribute__((ext_vector_type(4)));
-__device__ inline void slab_st4(float* p, slab_f4 v) {
-#if SWARM_SLAB_MODE == 1
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-#elif SWARM_SLAB_MODE == 3
-  __builtin_nontemporal_store(v, reinterpret_cast<slab_f4*>(p));
-#else
-  *reinterpret_cast<slab_f4*>(p) = v;
-#endif
-}
+// gradient-slab store (read once by the next launch, from another XCD).  The 4-B stores stay plain:
+// as nt (td 8.4 vs 8.0 us) and as 4-B write-through sc1 (9.5 us; round 6 again: +0.1-0.2 us per
+// tick) they cost more; the dW1 / dW2 tiles' 16-B pieces are write-through (sst4)
+__device__ inline void slab_st(float* p, float v) { *p = v; }
 #ifndef SWARM_DIAG_FEWSLABS
 #define SWARM_DIAG_FEWSLABS 0   // diagnostic builds only: > 0 = only the first K TD blocks store slabs (timing bound)
 #endif
@@ -223,37 +195,20 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #else
   auto sst_g = [&](int q, float v) { slab_st(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v); };
 #endif
-#if SWARM_B2_T   // 16-B stores of four consecutive parameters q .. q + 3 (q % 4 == 0, one slab run)
+// the dW1 / dW2 tiles' 16-B pieces: four consecutive parameters q .. q + 3 (q % 4 == 0) of one
+// 16-column slab run, stored write-through (swarm_common.h st16_wt): the 1,312 of a slab's 1,674
+// floats leave the XCD's L2 as they are written instead of at the launch end (round 6: C2 -0.22,
+// C3 -0.43 us per tick, profiles/r06_ab_b2t_v3_*.jsonl; plain 16-B stores were neutral)
   static_assert(OFF_W1 % 16 == 0 && OFF_W2 % 16 == 0 && kHidden % 16 == 0, "16-B slab pieces");
-  bool ho_block = false;   // the block holds a graph of this tick's slot (set with `pre` below)
-  (void)ho_block;
   auto sst4 = [&](int q, f32x4 v) {
-    float* const ptr = slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15));
-    const slab_f4 x = {v[0], v[1], v[2], v[3]};
-#if SWARM_B2_T == 4   // write-through in blocks off the hand-off chain, plain in the blocks on it
-    if (!ho_block) st16_wt(ptr, x[0], x[1], x[2], x[3]);
-    else *reinterpret_cast<slab_f4*>(ptr) = x;
-#elif SWARM_B2_T == 2
-    st16_wt(ptr, x[0], x[1], x[2], x[3]);   // swarm_common.h: write-through, hazard-padded
-#elif SWARM_B2_T == 3   // two compiler-generated 8-B write-through stores (agent-scope relaxed atomics)
-    typedef __attribute__((address_space(1))) unsigned long long g64;
-    const unsigned long long lo = ((unsigned long long)__float_as_uint(x[1]) << 32) | __float_as_uint(x[0]);
-    const unsigned long long hi = ((unsigned long long)__float_as_uint(x[3]) << 32) | __float_as_uint(x[2]);
-    __hip_atomic_store((g64*)ptr, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((g64*)(ptr + 2), hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    *reinterpret_cast<slab_f4*>(ptr) = x;
+#if SWARM_DIAG_FEWSLABS > 0
+    if (vb >= SWARM_DIAG_FEWSLABS) return;
+#elif SWARM_DIAG_FEWSLABS < 0
+    if (diag_skip) return;
 #endif
+    st16_wt(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v[0], v[1], v[2], v[3]);
   };
-#endif
-#if SWARM_SLAB_MODE
-  // the slab image: the target weights' LDS image, free once the block passed B1 (the target
-  // waves' forwards were its last readers); every slab element is written after B2
-  float* const slab_img = L.Ptg;
-  auto sst = [&](int q, float v) { slab_img[q] = v; };
-#else
   auto sst = sst_g;
-#endif
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
 
@@ -397,12 +352,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #endif
 #if SWARM_DIAG_FEWSLABS < 0
   diag_skip = (SWARM_DIAG_FEWSLABS == -1) == pre;
-#endif
-#if SWARM_B2_T
-  ho_block = pre;
-#endif
-#if SWARM_PRE_WARM   // A/B knob: every SWARM_PRE_WARM-th TD block also takes the pre path (warms its code)
-  pre = pre || (vb % SWARM_PRE_WARM) == 0;
 #endif
   pre = pre && online;
   const uint32_t tag = cc.tick + 1u;
@@ -726,7 +675,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 #pragma unroll
     for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(a2[s]));   // loaded unconditionally
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
-#if SWARM_B2_T
     // the transposed tiles (operands swapped: the same products, the same K order): lane (c, p)
     // holds dW1[out = c (+16)][in = 16 tj + 4p .. 4p + 3] and dW2[action = c][in = ...], four
     // consecutive parameters of one 16-column slab run, stored as ONE 16-B store per tile
@@ -739,20 +687,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
     sst4(OFF_W1 + c * kHidden + 16 * tj + 4 * p, d0);
     sst4(OFF_W1 + (16 + c) * kHidden + 16 * tj + 4 * p, d1);
     if (c < kActions) sst4(OFF_W2 + c * kHidden + 16 * tj + 4 * p, d2);
-#else
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      d0 = mfma16(a1[0][s], b1[s], d0);
-      d1 = mfma16(a1[1][s], b1[s], d1);
-      d2 = mfma16(an[s] == c ? a2[s] : 0.0f, b2v[s], d2);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sst(OFF_W1 + (4 * p + r) * kHidden + 16 * tj + c, d0[r]);
-      sst(OFF_W1 + (16 + 4 * p + r) * kHidden + 16 * tj + c, d1[r]);
-      if (4 * p + r < kActions) sst(OFF_W2 + (4 * p + r) * kHidden + 16 * tj + c, d2[r]);
-    }
-#endif
   };
   auto b2_job = [&](int job) {   // the vector sums: job 2 = db1, job 3 = db2 and the loss
     if (job == 2) {
@@ -993,15 +927,6 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
       }
     }
   }
-#if SWARM_SLAB_MODE
-  __syncthreads();   // B4: the block's slab image is complete
-  // 16-column runs of 64 B (column-block-major slab_index): quad i = columns 4i..4i+3 of column
-  // block i / 4; the run's padding columns (1674..1679) carry whatever the image holds there and
-  // are never read (the reduce reads columns <= N_PARAMS)
-  for (int i = threadIdx.x; i < kSlabQuads; i += NT)
-    slab_st4(slab_base + ((uint32_t)(i >> 2) * slab_stride + (uint32_t)((i & 3) * 4)),
-             reinterpret_cast<const slab_f4*>(slab_img)[i]);
-#endif
   SWARM_STAMP(7);
   SWARM_RTSTAMP(9);
 }
