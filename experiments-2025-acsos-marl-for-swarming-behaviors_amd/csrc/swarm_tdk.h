@@ -200,28 +200,14 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
 // floats leave the XCD's L2 as they are written instead of at the launch end (round 6: C2 -0.22,
 // C3 -0.43 us per tick, profiles/r06_ab_b2t_v3_*.jsonl; plain 16-B stores were neutral)
   static_assert(OFF_W1 % 16 == 0 && OFF_W2 % 16 == 0 && kHidden % 16 == 0, "16-B slab pieces");
-  auto wt16 = [&](int q, float a, float b, float c4, float d4) {   // parameters q .. q + 3, q % 4 == 0
+  auto sst4 = [&](int q, f32x4 v) {
 #if SWARM_DIAG_FEWSLABS > 0
     if (vb >= SWARM_DIAG_FEWSLABS) return;
 #elif SWARM_DIAG_FEWSLABS < 0
     if (diag_skip) return;
 #endif
-    st16_wt(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), a, b, c4, d4);
+    st16_wt(slab_base + ((uint32_t)(q >> 4) * slab_stride + (uint32_t)(q & 15)), v[0], v[1], v[2], v[3]);
   };
-  auto sst4 = [&](int q, f32x4 v) { wt16(q, v[0], v[1], v[2], v[3]); };
-#ifndef SWARM_WT_REST
-#define SWARM_WT_REST 0   // A/B knob: the vector sums and dW as 16-B write-through pieces too
-#endif
-#if SWARM_WT_REST
-  // lanes 4i .. 4i + 3 of a 16-lane row hold parameters q .. q + 3 (q % 4 == 0): lane 4i takes its
-  // three neighbours' values by DPP row shifts and stores the four as one write-through piece
-  auto wt_lanes4 = [&](int q, float v) {
-    const float v1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xF, 0xF, false));
-    const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x102, 0xF, 0xF, false));
-    const float v3 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x103, 0xF, 0xF, false));
-    if ((lane & 3) == 0) wt16(q, v, v1, v2, v3);
-  };
-#endif
   auto sst = sst_g;
   SWARM_RTSTAMP(8);
   SWARM_STAMP(0);
@@ -711,11 +697,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-#if SWARM_WT_REST
-        wt_lanes4(OFF_B1 + lane, acc);
-#else
         sst(OFF_B1 + lane, acc);
-#endif
       }
     } else if (lane < kActions || lane == 63) {   // db2 / loss: the ordered sum over the 32 rows,
       // 8 rows' reads at a time (each read unconditional: as selects around the reads they became
@@ -921,26 +903,10 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < kTdRows / 4; ++ks) acc = mfma16(ha[ks], xb[ks], acc);
-#if SWARM_WT_REST
-        // rows of 7 are not 16-B pieces: this job's 112 values (rows 16 t .. 16 t + 15) meet in LDS
-        // (the target image, free since B1; one region per job, each job one wave), then 28 lanes
-        // store them as 16-B write-through pieces
-        float* const scr = L.Ptg + 128 * t;
-        if (c < kFeat) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) scr[(4 * p + r) * kFeat + c] = acc[r];
-        }
-        wave_lds_sync();
-        if (lane < 16 * kFeat / 4) {
-          const float4 x = *reinterpret_cast<const float4*>(scr + 4 * lane);
-          wt16(OFF_W + 16 * kFeat * t + 4 * lane, x.x, x.y, x.z, x.w);
-        }
-#else
         if (c < kFeat) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) sst(OFF_W + (16 * t + 4 * p + r) * kFeat + c, acc[r]);
         }
-#endif
       } else if (job == 2) {   // att_src (half 0) / att_dst (half 1): sum_n da[n] H[n][col]
         const float* da = h == 0 ? TB.das : TB.dad;
         float v[kTdRows];
@@ -949,12 +915,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-#if SWARM_WT_REST
-        static_assert(OFF_ATT_SRC == 0 && OFF_ATT_DST == 32, "att_src / att_dst = parameters 0..63 = lanes");
-        wt_lanes4(lane, acc);
-#else
         sst((h == 0 ? OFF_ATT_SRC : OFF_ATT_DST) + col, acc);
-#endif
       } else if (lane < kHidden) {
         float v[kTdRows];
 #pragma unroll
@@ -962,11 +923,7 @@ __device__ __forceinline__ void td_body(TdSmem<NS>& L, const int vb, const int32
         float acc = v[0];
 #pragma unroll
         for (int n = 1; n < kTdRows; ++n) acc = acc + v[n];
-#if SWARM_WT_REST
-        wt_lanes4(OFF_BIAS + lane, acc);
-#else
         sst(OFF_BIAS + lane, acc);
-#endif
       }
     }
   }
