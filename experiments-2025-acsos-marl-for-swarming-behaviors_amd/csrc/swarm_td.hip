@@ -50,17 +50,6 @@ struct ReduceArgs {
 #ifndef SWARM_RED_GROUPS
 #define SWARM_RED_GROUPS 64   // test builds: 16 (256-thread blocks, so 8 ranks' peer reduces fit one GPU)
 #endif
-#ifndef SWARM_RED_COMP
-#define SWARM_RED_COMP 0   // A/B knob: the slab sum as an error-free (hi, lo) pair (TwoSum)
-#endif
-// s + v as an error-free transformation: s <- fl(s + v), lo <- lo + the rounding error of that add
-__device__ inline void two_sum_acc(float& s, float& lo, float v) {
-  const float t = s + v;
-  const float bv = t - s;
-  const float e = (s - (t - bv)) + (v - bv);
-  s = t;
-  lo = lo + e;
-}
 constexpr int kRedCols = 16;      // columns per reduce block
 constexpr int kRedGroups = SWARM_RED_GROUPS;   // slab groups per column (consecutive slabs each)
 constexpr int kRedRuns = kRedGroups / 8;
@@ -143,10 +132,6 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
                                                                             int n_slabs, int advance, ReduceArgs A) {
   __shared__ float part[kRedGroups][kRedCols];
   __shared__ float part2[kRedRuns][kRedCols];
-#if SWARM_RED_COMP
-  __shared__ float partl[kRedGroups][kRedCols];   // the low parts of the (hi, lo) slab sums
-  __shared__ float part2l[kRedRuns][kRedCols];
-#endif
   __shared__ float peer_rv[PEER ? SWARM_PEER_MAX : 1][kRedCols];
   __shared__ float sqv[kRedCols];
   SWARM_RTSTAMP(22);
@@ -179,43 +164,6 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
 #pragma unroll
   for (int j = 0; j < kChunk; ++j)
     v0[j] = (col <= N_PARAMS && b0 + j < b1) ? scol[(uint32_t)(b0 + j) * kSlabCols] : 0.0f;
-#if SWARM_RED_COMP
-  // the slab sum as an error-free (hi, lo) pair: TwoSum per added slab, the low parts summed apart
-  // and the pairs combined the same way up the fixed two-level tree; the column's gradient is
-  // hi + lo, within about one rounding of the exact sum of the slabs (-ffp-contract=off keeps the
-  // TwoSum steps exact)
-  float s = v0[0], sl = 0.0f;
-#pragma unroll
-  for (int j = 1; j < kChunk; ++j) two_sum_acc(s, sl, v0[j]);
-  if (col <= N_PARAMS) {
-    for (int b = b0 + kChunk; b < b1; b += kChunk) {
-      float v[kChunk];
-#pragma unroll
-      for (int j = 0; j < kChunk; ++j) v[j] = (b + j < b1) ? scol[(uint32_t)(b + j) * kSlabCols] : 0.0f;
-#pragma unroll
-      for (int j = 0; j < kChunk; ++j) two_sum_acc(s, sl, v[j]);
-    }
-  }
-  SWARM_STAMP(29);
-  part[q][c] = s;
-  partl[q][c] = sl;
-  __syncthreads();
-  SWARM_STAMP(30);
-  if (q < kRedRuns) {
-    float r = part[8 * q][c], rl = partl[8 * q][c];
-#pragma unroll
-    for (int gi = 1; gi < 8; ++gi) { two_sum_acc(r, rl, part[8 * q + gi][c]); rl = rl + partl[8 * q + gi][c]; }
-    part2[q][c] = r;
-    part2l[q][c] = rl;
-  }
-  __syncthreads();
-  float gcol = 0.0f;   // q == 0: this column's gradient as written to grad
-  if (q == 0 && col <= N_PARAMS) {
-    float tot = part2[0][c], totl = part2l[0][c];
-#pragma unroll
-    for (int gi = 1; gi < kRedRuns; ++gi) { two_sum_acc(tot, totl, part2[gi][c]); totl = totl + part2l[gi][c]; }
-    tot = tot + totl;
-#else
   float s = v0[0];
 #pragma unroll
   for (int j = 1; j < kChunk; ++j) s = s + v0[j];
@@ -244,7 +192,6 @@ __global__ __launch_bounds__(kRedCols * kRedGroups) void grad_reduce_kernel(cons
     float tot = part2[0][c];
 #pragma unroll
     for (int gi = 1; gi < kRedRuns; ++gi) tot = tot + part2[gi][c];
-#endif
     if (PEER) part[0][c] = tot;   // part[0] is free again: this rank's column sums
     else A.grad[col] = tot;
     gcol = tot;
