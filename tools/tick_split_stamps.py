@@ -25,9 +25,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["SWARM_LIB_PATH"] = os.path.join(ROOT, "experiments-2025-acsos-marl-for-swarming-behaviors_amd",
-                                            "libswarm_hip_stamps.so" if "--lib=stamps" in sys.argv
-                                            else "libswarm_hip_rtstamps.so")
+# SWARM_SPLIT_LIB: a prebuilt realtime-stamps library to run instead (e.g. a diagnostic worktree's)
+os.environ["SWARM_LIB_PATH"] = os.environ.get("SWARM_SPLIT_LIB") or os.path.join(
+    ROOT, "experiments-2025-acsos-marl-for-swarming-behaviors_amd",
+    "libswarm_hip_stamps.so" if "--lib=stamps" in sys.argv else "libswarm_hip_rtstamps.so")
 sys.argv = [a for a in sys.argv if not a.startswith("--lib=")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -95,6 +96,15 @@ def main():
         rows.append({"tick_span_us": (k1 - k0) / 100, "tick_to_reduce_gap_us": (r0 - k1) / 100,
                      "reduce_span_us": (r1 - r0) / 100, "act_waves_us": (a1 - a0) / 100,
                      "td_waves_us": (d1 - d0) / 100})
+        # per block kind, when the library stamps the control and copy-back blocks' exits too: the
+        # last exit of the column blocks, the control block and the copy-back blocks after r0
+        ncol = RED_BLOCKS - 4
+        kinds = {"columns": r[:ncol], "control": r[ncol:ncol + 1], "copy_back": r[ncol + 1:RED_BLOCKS]}
+        for name, rr in kinds.items():
+            a = rr.reshape(-1, 32).astype(np.int64)
+            a = a[(a[:, 22] > 0) & (a[:, 23] > 0)]
+            if len(a):
+                rows[-1][f"reduce_{name}_end_us"] = (int(a[:, 23].max()) - r0) / 100
         # [tick, reduce, tick]: the reduce slots hold the middle launch, the tick slots the last
         tbuf.zero_()
         rbuf.zero_()
@@ -116,7 +126,7 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         per.append(e0.elapsed_time(e1) * 1e3 / 100)
-    med = {k: float(np.median([r[k] for r in rows])) for k in rows[0]}
+    med = {k: float(np.median([r[k] for r in rows if k in r])) for k in rows[0]}
     med["reduce_to_tick_gap_us"] = float(np.median(gap_rt))
     med["sum_us"] = med["tick_span_us"] + med["tick_to_reduce_gap_us"] + med["reduce_span_us"] + med["reduce_to_tick_gap_us"]
     med["tick_period_chain_us (HIP events, this library)"] = float(np.median(per))
