@@ -34,6 +34,7 @@ trained weights (``data/models/*.pth``), committed as fixtures under
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass
 
@@ -878,6 +879,28 @@ def _td_loss_grad_gcn(flat_params, flat_target, s_state, actions, rewards, s_nex
     grad = torch.cat([(params[k].grad if params[k].grad is not None else torch.zeros_like(params[k])).reshape(-1)
                       for k, _ in PARAM_ORDER]).clone()
     return float(loss.item()), grad, values.detach().squeeze(1), target
+
+
+@contextlib.contextmanager
+def correctly_rounded_linears():
+    """Inside this context every F.linear of the restatement (the GAT / GCN lin, lin1 and lin2, and
+    autograd's products for them) is evaluated in float64 and rounded once to fp32: a further fp32
+    evaluation of the same function that differs from torch's only in each dot product's rounding,
+    i.e. in Q's last bits.  Test infrastructure: it measures how far a legitimate fp32 forward moves
+    the gradient (tools/fwd_rounding.py, tests/test_gpu_parity_large.py records)."""
+    lin0 = F.linear
+
+    def lin_cr(x, w, b=None):
+        y = x.double() @ w.double().t()
+        if b is not None:
+            y = y + b.double()
+        return y.to(x.dtype)
+
+    F.linear = lin_cr
+    try:
+        yield
+    finally:
+        F.linear = lin0
 
 
 def clip_adam(flat_params, grad, adam_m, adam_v, adam_step: int, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,

@@ -283,6 +283,33 @@ def test_td_step_oracle_reduces_loss(golden_weights):
     assert losses[-1] < losses[0]
 
 
+@pytest.mark.parametrize("conv", ["gat", "gcn"])
+def test_correctly_rounded_linears_evaluation(golden_weights, conv):
+    """The fifth fp32 evaluation the large parity tests record (oracle.correctly_rounded_linears):
+    every Q of it is within one fp32 ulp of the float64 evaluation's (observed <= 0.78 ulp; torch's fp32
+    Q up to 3.7 ulp), its gradient is fp32, and leaving the context restores torch's F.linear."""
+    p = torch.tensor(golden_weights["obstacle_avoidance"][5])
+    t = torch.tensor(golden_weights["obstacle_avoidance"][6])
+    g = torch.Generator().manual_seed(1)
+    S, N = 16, 7
+    s = torch.cat([torch.rand(S, N, 2, generator=g) * 2 - 1, torch.randn(S, N, 2, generator=g) * 0.1], -1)
+    s1 = s + torch.randn(S, N, 4, generator=g) * 0.01
+    a = torch.randint(0, 9, (S, N), generator=g)
+    r = torch.randn(S, N, generator=g)
+    lin0 = torch.nn.functional.linear
+    _, g32, q32, _ = O.td_loss_grad(p, t, s, a, r, s1, conv=conv)
+    with O.correctly_rounded_linears():
+        assert torch.nn.functional.linear is not lin0
+        _, gcr, qcr, _ = O.td_loss_grad(p, t, s, a, r, s1, conv=conv)
+    assert torch.nn.functional.linear is lin0
+    _, _, q64, _ = O.td_loss_grad(p, t, s, a, r, s1, conv=conv, dtype=torch.float64)
+    assert gcr.dtype == torch.float32 and qcr.dtype == torch.float32
+    ulp = torch.from_numpy(np.spacing(np.abs(q64.numpy()).astype(np.float32)).astype(np.float64))
+    e_cr, e_32 = (qcr.double() - q64).abs() / ulp, (q32.double() - q64).abs() / ulp
+    assert float(e_cr.max()) <= 1.0 and float(e_cr.mean()) < float(e_32.mean())
+    assert torch.allclose(gcr, g32, rtol=1e-3, atol=1e-5)
+
+
 def test_gcn_module_state_dict_matches_reference_layout(golden_weights):
     import swarm_amd
     model = swarm_amd.GCN(7, 32, 9)
