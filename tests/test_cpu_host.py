@@ -35,6 +35,15 @@ def test_library_exports_every_header_symbol():
     assert lib.swarm_abi_version() == L.ABI_VERSION == 10 and lib.swarm_n_params() == O.N_PARAMS
 
 
+def test_integration_guide_names_every_entry_point():
+    """INTEGRATION.md §3 says where each C entry point plugs into the reference: every symbol
+    include/swarm_hip.h declares appears there."""
+    hdr = open(os.path.join(ROOT, "include", "swarm_hip.h")).read()
+    names = set(re.findall(r"^\s*(?:int|int64_t|uint32_t|const char\*)\s+(swarm_\w+)\(", hdr, re.M))
+    guide = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert sorted(n for n in names if f"`{n}" not in guide and f"{n}`" not in guide) == []
+
+
 def test_topk_emulation_matches_torch_fixture():
     z = np.load(os.path.join(ROOT, "tests", "golden", "topk_ties.npz"))
     for row, (n, k), s in zip(z["dist"], z["nk"], z["sets"]):
