@@ -2,6 +2,7 @@
 # Round 6: interleaved A/B of the slab-store modes (SWARM_SLAB_MODE, tools/ab_build.py variants)
 # at C2, C3 and C5's N = 12 shard, then the instruction-fetch counters of base and preall, each
 # counter set in its own rocprofv3 pass.  Stops at the first failure.
+# NOTE: the SWARM_SLAB_MODE knob was removed after this A/B (642ba79); its sources are at b67f329, so rebuilding the variants from today's tree builds the product library.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 V=${V:-"base slabsc1 slabplain4 slabnt4"}

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6: the slab's remaining pieces (vector sums by DPP lane gathers, dW rows through LDS) as 16-B
 # write-through stores too (SWARM_WT_REST): bit for bit against the in-tree library, then the A/B.
+# NOTE: the SWARM_WT_REST knob was removed after this A/B (ce97a8a); its sources are at 6f7b431, so rebuilding the variants from today's tree builds the product library.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 : > gpurun_out/r06_bitcmp5.jsonl
