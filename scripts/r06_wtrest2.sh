@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6: the slab's remaining pieces as 16-B write-through stores in the blocks holding none of this
 # tick's transitions only (SWARM_WT_REST=2): bit for bit against the in-tree library, then the A/B.
-# NOTE: SWARM_WT_REST=2 was the 6f7b431 knob plus a block-uniform switch; removed after this A/B (49d2423), so rebuilding the variants from today's tree builds the product library.
+# NOTE: the SWARM_WT_REST=2 sources are scripts/patches/r06_wtrest2.patch (git apply, then tools/ab_build.py
+# wtrest2=-DSWARM_WT_REST=2); the knob is not in the tree, so without the patch the variant is the product library.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 : > gpurun_out/r06_bitcmp6.jsonl
