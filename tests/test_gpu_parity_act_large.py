@@ -30,6 +30,8 @@ CASES = [("C2", "GoTo", 8, 1024, "gat"), ("C3", "ObstacleAvoidance", 12, 1024, "
          ("C5 N=5 GCN", "ObstacleAvoidance", 5, 512, "gcn"), ("C5 N=12 GCN", "ObstacleAvoidance", 12, 512, "gcn")]
 # C5's sweep interior (VERDICT r5 "next" #1): every agent count from 5 to 12, GAT and GCN
 CASES += [(f"C5 N={n} {conv.upper()}", "ObstacleAvoidance", n, 512, conv) for n in (6, 7, 8, 9, 10, 11) for conv in ("gat", "gcn")]
+# the GCN variant (a13) at C2's and C3's full 1,024-env shapes too (the sweep's "C2 GCN train" line)
+CASES += [("C2 GCN", "GoTo", 8, 1024, "gcn"), ("C3 GCN", "ObstacleAvoidance", 12, 1024, "gcn")]
 SCEN = {"GoTo": O.SCENARIO_GOTO, "ObstacleAvoidance": O.SCENARIO_OA}
 EPS, SEED = 0.3, 21
 

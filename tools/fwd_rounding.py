@@ -1,8 +1,9 @@
 """Diagnostic (CPU only): how far a legitimate fp32 FORWARD moves the TD gradient, against the
-per-tensor bound of tests/test_gpu_parity_large.py.
+per-tensor bound tests/test_gpu_parity_large.py had until round 6's last change.
 
-That bound is 4x "the fp32 oracle's own error": the largest distance to the float64 evaluation of
-four fp32 evaluations (the batch in three orders, and the other formulation).  Three of the four
+That bound was 4x "the fp32 oracle's own error": the largest distance to the float64 evaluation of
+four fp32 evaluations (the batch in three orders, and the other formulation); the evaluation below
+is now the fifth member of that spread.  Three of the four
 share torch's rounding of every per-node dot product, so Q's last bits, which the TD error
 delta = Q - y amplifies (|Q| ~ 10^2, |delta| ~ 1), are nearly the same in all of them.  This tool
 adds a fifth evaluation that differs only there: every linear layer correctly rounded
