@@ -887,7 +887,10 @@ def correctly_rounded_linears():
     autograd's products for them) is evaluated in float64 and rounded once to fp32: a further fp32
     evaluation of the same function that differs from torch's only in each dot product's rounding,
     i.e. in Q's last bits.  Test infrastructure: it measures how far a legitimate fp32 forward moves
-    the gradient (tools/fwd_rounding.py, tests/test_gpu_parity_large.py records)."""
+    the gradient (tools/fwd_rounding.py), and it is the fifth member of the gradient bound's fp32
+    spread (tests/test_gpu_parity_large.py oracle_grad_orders).  It replaces
+    torch.nn.functional.linear process-wide while the context is open (restored on exit, also on an
+    exception), so it is not for use beside other threads calling torch."""
     lin0 = F.linear
 
     def lin_cr(x, w, b=None):
